@@ -1,0 +1,230 @@
+/*
+ * optflow.h — C ABI of the MI355X-native variational optical-flow solver.
+ *
+ * One shared library (liboptflow.so, HIP for gfx950) runs the reference's
+ * coarse-to-fine IRLS inner loop on the GPU.  The Python package
+ * `optical_flow` (same API as jordanshivers/optical-flow-python) binds these
+ * symbols with ctypes; any other host language binds the same symbols (see
+ * INTEGRATION.md).  No torch / CUDA types appear here: plain pointers, sizes
+ * and POD structs only.
+ *
+ * Conventions
+ *   - Host buffers are caller-owned, C-contiguous float32.  "planar" means
+ *     channel-major: plane c of an HxW image starts at c*H*W.  Flow fields
+ *     (uv) are planar too: u plane then v plane.
+ *   - Every function returns 0 on success and a negative OF_E* code on error;
+ *     of_last_error() returns a message for the calling thread's context.
+ *   - A context binds one HIP device and one stream; one context per host
+ *     thread.  Calls are synchronous with respect to host buffers.
+ *   - Non-convergence of an iterative solve is reported (of_stats), never an
+ *     error — matching the reference, which ignores cg's `info`
+ *     (optical_flow/methods/base.py:134-136).
+ */
+#ifndef OPTFLOW_H
+#define OPTFLOW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OF_ABI_VERSION 1
+
+/* status codes */
+#define OF_OK 0
+#define OF_EINVAL (-1)   /* bad argument (ValueError in the Python mirror) */
+#define OF_EHIP (-2)     /* HIP runtime error */
+#define OF_ENOMEM (-3)
+#define OF_ENOTSUP (-4)  /* valid in the reference but not supported here */
+#define OF_ERCCL (-5)
+
+/* method kinds: optical_flow/methods/{hs,ba,classic_nl,alt_ba}.py */
+enum of_method { OF_METHOD_HS = 0, OF_METHOD_BA = 1, OF_METHOD_CLASSIC_NL = 2, OF_METHOD_ALT_BA = 3 };
+
+/* interpolation_method (optical_flow/utils/derivatives.py:148-294) */
+enum of_interp { OF_INTERP_CUBIC = 0 /* 'cubic' = cubic B-spline */,
+                 OF_INTERP_BICUBIC = 1 /* 'bi-cubic' = Hermite */,
+                 OF_INTERP_BILINEAR = 2 /* 'bi-linear' */ };
+
+/* solver (optical_flow/methods/base.py:87-114) */
+enum of_solver { OF_SOLVER_BACKSLASH = 0, OF_SOLVER_PCG = 1, OF_SOLVER_SOR = 2 };
+
+/* robust penalties (optical_flow/robust/penalties.py); OF_PEN_CONST is an
+ * internal kind: rho'(x)/x == p0 everywhere (Horn-Schunck's 1/sigma^2). */
+enum of_penalty_kind {
+  OF_PEN_QUADRATIC = 0, OF_PEN_LORENTZIAN = 1, OF_PEN_CHARBONNIER = 2,
+  OF_PEN_GEN_CHARBONNIER = 3, OF_PEN_GEMAN_MCCLURE = 4, OF_PEN_HUBER = 5,
+  OF_PEN_TUKEY = 6, OF_PEN_GAUSSIAN = 7, OF_PEN_TDIST = 8, OF_PEN_TDIST_UNNORM = 9,
+  OF_PEN_CONST = 100
+};
+
+typedef struct of_penalty {
+  int32_t kind;
+  int32_t pad_;
+  double p0;   /* sigma, or r for t-dist */
+  double p1;   /* a for generalized charbonnier, s for t-dist */
+} of_penalty;
+
+/*
+ * POD mirror of the method object's attribute bag
+ * (optical_flow/methods/base.py:21-63, hs.py:23-47, ba.py:26-55,
+ *  classic_nl.py:32-87, alt_ba.py:31-79).  The Python mirror fills it.
+ */
+typedef struct of_params {
+  int32_t method;            /* enum of_method */
+  int32_t solver;            /* enum of_solver */
+  int32_t interp;            /* enum of_interp */
+  int32_t texture;           /* ROF structure-texture pre-pass */
+  int32_t fc;                /* high-pass pre-filter */
+  int32_t auto_level;        /* BA/NL: pyramid_levels from image size */
+  int32_t pyramid_levels;
+  int32_t gnc_iters;
+  int32_t gnc_pyramid_levels;
+  int32_t max_iters;         /* IRLS warping iterations (BA, NL, AltBA) */
+  int32_t max_warping_iters; /* HS */
+  int32_t max_linear;
+  int32_t pcg_maxiter;
+  int32_t sor_max_iters;
+  int32_t limit_update;
+  int32_t median_filter_size;   /* 0 = None, else odd square size (5) */
+  int32_t mf_iter;              /* HS */
+  int32_t use_wmf;              /* Classic+NL non-local weighted median */
+  int32_t area_hsz;
+  int32_t itersLO;              /* AltBA */
+  int32_t exact_maxiter;        /* 'backslash' surrogate: max PCG iterations */
+  int32_t display;
+  int32_t guide_mode;           /* estimate_flow builds a colour guide (color_images is not None) */
+  int32_t pad_;
+  double lambda_;
+  double lambda_q;
+  double alpha;                 /* initial GNC alpha */
+  double pyramid_spacing;
+  double gnc_pyramid_spacing;
+  double pcg_rtol;
+  double exact_rtol;            /* 'backslash' surrogate tolerance */
+  double sor_omega;
+  double sor_tol;
+  double blend;
+  double alp;
+  double sigma_i;
+  double sigmaD2, sigmaS2;      /* HS */
+  double lambda2, lambda3;      /* AltBA */
+  double deriv_filter[5];
+  of_penalty rho_data, rho_spatial_u[2], rho_spatial_v[2];
+  of_penalty qua_data, qua_spatial_u[2], qua_spatial_v[2];  /* quadratic relaxation */
+  of_penalty rho_couple;        /* AltBA */
+} of_params;
+
+/* per-call statistics (may be NULL) */
+#define OF_MAX_LEVELS 32
+typedef struct of_stats {
+  int32_t n_levels;                  /* levels processed (all GNC stages) */
+  int32_t level_h[OF_MAX_LEVELS];
+  int32_t level_w[OF_MAX_LEVELS];
+  int32_t level_stage[OF_MAX_LEVELS];
+  double level_ms[OF_MAX_LEVELS];    /* wall time of one compute_flow_base */
+  int32_t solves;
+  int32_t solver_iters_total;
+  int32_t solver_iters_max;
+  int32_t solves_not_converged;
+  double total_ms;
+  double preprocess_ms;
+} of_stats;
+
+typedef struct of_ctx of_ctx;
+
+/* ---- context ---- */
+int of_abi_version(void);
+int of_device_count(int *count);
+int of_ctx_create(int device, of_ctx **out);
+int of_ctx_destroy(of_ctx *ctx);
+const char *of_last_error(of_ctx *ctx);
+int of_synchronize(of_ctx *ctx);
+/* per-kernel HIP-event timing on the ctx stream (0 = off); see of_kernel_times */
+int of_set_profiling(of_ctx *ctx, int enable);
+/* kernel timing accumulated since enable: names[i] (static strings), ms[i], count[i] */
+int of_kernel_times(of_ctx *ctx, int max, const char **names, double *ms, int64_t *count, int *n);
+
+/*
+ * Whole pair: estimate_flow (optical_flow/interface.py:11-71) without its
+ * Python-side parameter handling.
+ *   im1, im2 : H x W x C interleaved float32, C == 1 (gray) or C == 3 (RGB;
+ *              converted on device with _rgb2gray / _rgb2lab semantics)
+ *   init_uv  : planar 2 x H x W or NULL (zeros)
+ *   out_uv   : planar 2 x H x W
+ * The final GNC alpha is written back to params->alpha (Classic+NL keeps it,
+ * classic_nl.py:180-184; BA restores it, ba.py:136).
+ */
+int of_estimate_flow(of_ctx *ctx, of_params *params, const float *im1, const float *im2,
+                     int H, int W, int C, const float *init_uv, float *out_uv, of_stats *stats);
+
+/*
+ * compute_flow() on an already preprocessed pair (the method object's
+ * `images`, `color_images`):
+ *   images : planar (2*nc) x H x W   (frame-1 channels then frame-2 channels)
+ *   guide  : planar gc x H x W Lab/gray guide for the weighted median, or NULL
+ */
+int of_compute_flow(of_ctx *ctx, of_params *params, const float *images, int H, int W, int nc,
+                    const float *guide, int gc, const float *init_uv, float *out_uv, of_stats *stats);
+
+/* compute_flow_base() for one pyramid level with the given alpha (one call =
+ * all warping iterations of the level; hs.py:109-142, ba.py:143-206,
+ * classic_nl.py:200-277).  uv_in / out_uv planar 2 x H x W. */
+int of_compute_flow_base(of_ctx *ctx, of_params *params, const float *images, int H, int W, int nc,
+                         const float *guide, int gc, double alpha, const float *uv_in, float *out_uv);
+
+/* ---- device-resident batch path (benchmark / multi-GPU sharding) ---- */
+/* upload one RGB/gray pair into slot `slot` of the ctx (H2D, untimed) */
+int of_pair_upload(of_ctx *ctx, int slot, const float *im1, const float *im2, int H, int W, int C);
+/* run estimate_flow on device-resident slot; result stays on device */
+int of_pair_run(of_ctx *ctx, int slot, of_params *params, of_stats *stats);
+/* D2H of a slot's flow (planar 2 x H x W) */
+int of_pair_download(of_ctx *ctx, int slot, float *out_uv);
+
+/* ---- RCCL gather of device-resident results (one process per GPU) ---- */
+int of_rccl_unique_id(char *out128);
+int of_rccl_init(of_ctx *ctx, const char *id128, int nranks, int rank);
+/* gather `nslots` flows (slots 0..nslots-1 of every rank) to rank 0; rank 0's
+ * out_uv receives nranks*nslots planar flows (may be NULL on other ranks) */
+int of_rccl_gather_flows(of_ctx *ctx, int nslots, float *out_uv_rank0);
+int of_rccl_finalize(of_ctx *ctx);
+
+/* ---- stage entries (one per hot-path row of SURVEY.md §8a; parity tests) ---- */
+/* _rgb2gray + _rgb2lab + per-channel scale_image (interface.py:49-64,74-141) */
+int of_preprocess(of_ctx *ctx, const float *rgb1, const float *rgb2, int H, int W,
+                  float *gray_pair /*2xHxW*/, float *lab /*3xHxW*/);
+/* structure_texture_decomposition_rof (utils/image_processing.py:52-136) */
+int of_rof_texture(of_ctx *ctx, const float *im, int H, int W, int C, double theta, int iters,
+                   double alp, float *out);
+/* compute_image_pyramid level l+1 from level l (utils/pyramid.py:44-73) */
+int of_pyramid_level(of_ctx *ctx, const float *im, int H, int W, int C, const double *kern, int ksize,
+                     double ratio, float *out, int *outH, int *outW);
+/* resample_flow (utils/warping.py:6-45) */
+int of_resample_flow(of_ctx *ctx, const float *uv, int H, int W, int nH, int nW, float *out);
+/* partial_deriv (utils/derivatives.py:148-296): images planar 2*nc */
+int of_partial_deriv(of_ctx *ctx, const float *images, int H, int W, int nc, const float *uv,
+                     int interp, const double *deriv_filter, double blend,
+                     float *It, float *Ix, float *Iy);
+/* flow_operator, matrix-free (classic_nl.py:279-378, ba.py:208-302, hs.py:144-203):
+ * coef = 7 planes {wx_u, wy_u, wx_v, wy_v, a_uu, a_uv, a_vv}, rhs = planes {b_u, b_v}.
+ * wx_* / wy_* are the (lambda-scaled) weights of the edge to the right / below. */
+int of_flow_operator(of_ctx *ctx, const of_params *params, double alpha, const float *uv,
+                     const float *duv, const float *It, const float *Ix, const float *Iy,
+                     int H, int W, int nc, float *coef, float *rhs);
+/* _solve_linear_system (base.py:87-172) on the matrix-free operator */
+int of_solve(of_ctx *ctx, const of_params *params, const float *coef, const float *rhs, int H, int W,
+             float *x, int *iters, double *rel_residual);
+/* detect_occlusion (utils/occlusion.py:6-56) */
+int of_detect_occlusion(of_ctx *ctx, const float *uv, const float *images, int H, int W, int nc,
+                        float *occ);
+/* denoise_color_weighted_medfilt2 (utils/weighted_median.py:24-112) */
+int of_weighted_median(of_ctx *ctx, const float *uv, const float *guide, int gc, const float *occ,
+                       int H, int W, int area_hsz, double sigma_i, float *out);
+/* scipy.ndimage.median_filter(size, mode='reflect') on each of `planes` planes */
+int of_median_filter(of_ctx *ctx, const float *in, int H, int W, int planes, int size, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPTFLOW_H */

@@ -1,0 +1,179 @@
+// common.h — shared device helpers for liboptflow (gfx950 / CDNA4).
+//
+// Data layout in HBM (DESIGN.md §"Data layout"): every image plane is fp32
+// row-major with a row pitch padded to a multiple of 64 floats (256 B), so a
+// wave64 reads one aligned 256-B row segment per plane.  Flow-like vector
+// fields (uv, PCG vectors) are float2 {u, v} per pixel with the same pitch.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "optflow.h"
+
+#define OF_WAVE 64
+#define OF_BX 64  // block x = one wave across a row
+#define OF_BY 4   // 4 rows per block -> 256 threads
+
+static inline int of_pitch(int W) { return (W + 63) & ~63; }
+
+// ---- boundary extensions -------------------------------------------------
+// scipy.ndimage mode='reflect' (half-sample symmetric: d c b a | a b c d)
+__device__ __forceinline__ int ext_reflect(int i, int n) {
+  if (n == 1) return 0;
+  int p = 2 * n;
+  i %= p;
+  if (i < 0) i += p;
+  return i < n ? i : p - 1 - i;
+}
+// np.pad 'reflect' / scipy 'mirror' (whole-sample: d c b | a b c d)
+__device__ __forceinline__ int ext_mirror(int i, int n) {
+  if (n == 1) return 0;
+  int p = 2 * (n - 1);
+  i %= p;
+  if (i < 0) i += p;
+  return i < n ? i : p - i;
+}
+__device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? lo : (i > hi ? hi : i); }
+
+// ---- robust penalty weights rho'(x)/x (penalties.py d_type == 2) ---------
+struct PenF {
+  int kind;
+  float p0, p1;
+};
+
+__host__ static inline PenF to_penf(const of_penalty &p) {
+  PenF q;
+  q.kind = p.kind;
+  q.p0 = (float)p.p0;
+  q.p1 = (float)p.p1;
+  return q;
+}
+
+__device__ __forceinline__ float pen_w(const PenF &p, float x) {
+  switch (p.kind) {
+    case OF_PEN_QUADRATIC: return 2.0f / (p.p0 * p.p0);
+    case OF_PEN_LORENTZIAN: return 2.0f / (2.0f * p.p0 * p.p0 + x * x);
+    case OF_PEN_CHARBONNIER: {
+      float s2 = p.p0 * p.p0, t = x / s2;
+      return 1.0f / (s2 * sqrtf(1.0f + t * t));
+    }
+    case OF_PEN_GEN_CHARBONNIER: return 2.0f * p.p1 * powf(p.p0 * p.p0 + x * x, p.p1 - 1.0f);
+    case OF_PEN_GEMAN_MCCLURE: {
+      float s2 = p.p0 * p.p0, d = s2 + x * x;
+      return 2.0f * s2 / (d * d);
+    }
+    case OF_PEN_HUBER: {
+      float s2 = p.p0 * p.p0, ax = fabsf(x);
+      return ax <= s2 ? 2.0f : 2.0f * s2 / fmaxf(ax, 1e-30f);
+    }
+    case OF_PEN_TUKEY: {
+      float s2 = p.p0 * p.p0, om = 1.0f - x * x / s2;
+      return fabsf(x) <= p.p0 ? 2.0f * om * om / s2 : 0.0f;
+    }
+    case OF_PEN_GAUSSIAN: return 1.0f / (p.p0 * p.p0);
+    case OF_PEN_TDIST:
+    case OF_PEN_TDIST_UNNORM: return (p.p0 + 1.0f) / (p.p1 * p.p1 * p.p0 + x * x);
+    default: return p.p0;  // OF_PEN_CONST
+  }
+}
+
+// ---- order-preserving float <-> uint32 (sorting, atomic min/max) ----------
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t o) {
+  uint32_t b = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  return __uint_as_float(b);
+}
+
+// ---- reductions -----------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// Sum NV doubles over the block (256 threads max); result valid in thread 0.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *lds /* NV*16 */) {
+  const int tid = threadIdx.x + threadIdx.y * blockDim.x;
+  const int nw = (blockDim.x * blockDim.y + 63) / 64;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[k * 16 + (tid >> 6)] = v[k];
+  __syncthreads();
+  if (tid == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double s = 0;
+      for (int w = 0; w < nw; ++w) s += lds[k * 16 + w];
+      v[k] = s;
+    }
+}
+
+// Last-block-done hand-off (cdna_hip_programming.md §6 Guideline 16):
+// thread 0 stores the block partials, releases at agent scope and takes a
+// ticket; the block drawing nblocks-1 acquires and may read every partial.
+template <int NV>
+__device__ __forceinline__ bool arrive_last(const double (&v)[NV], double *partials, unsigned *counter, int nblocks,
+                                            int bid) {
+  __shared__ int s_last;
+  const int tid = threadIdx.x + threadIdx.y * blockDim.x;
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) partials[(size_t)k * nblocks + bid] = v[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = prev == (unsigned)(nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// In the last block: fixed-order sum of NV partial arrays (deterministic).
+template <int NV>
+__device__ __forceinline__ void final_sum(double (&out)[NV], const double *partials, int nblocks, double *lds) {
+  const int tid = threadIdx.x + threadIdx.y * blockDim.x;
+  const int nt = blockDim.x * blockDim.y;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = 0;
+    for (int b = tid; b < nblocks; b += nt) s += partials[(size_t)k * nblocks + b];
+    out[k] = s;
+  }
+  __syncthreads();
+  block_sum<NV>(out, lds);
+}
+
+// ---- launch geometry: 64x4 blocks, grid-stride over row groups ----------
+struct Grid2 {
+  dim3 grid, block;
+  int nblocks;
+};
+static inline Grid2 grid2(int H, int W, int max_blocks = 2048) {
+  Grid2 g;
+  g.block = dim3(OF_BX, OF_BY, 1);
+  int gx = (W + OF_BX - 1) / OF_BX;
+  int gy = (H + OF_BY - 1) / OF_BY;
+  int cap = max_blocks / gx;
+  if (cap < 1) cap = 1;
+  if (gy > cap) gy = cap;
+  g.grid = dim3(gx, gy, 1);
+  g.nblocks = gx * gy;
+  return g;
+}
+
+// pixel loop of a grid2 launch: for (i...) rows, j column
+#define OF_FOR_PIXELS(H, W)                                        \
+  const int j = blockIdx.x * OF_BX + threadIdx.x;                  \
+  for (int i = blockIdx.y * OF_BY + threadIdx.y; i < (H); i += gridDim.y * OF_BY)

@@ -1,0 +1,1320 @@
+// driver.hip — liboptflow.so: C ABI (include/optflow.h) + the on-device
+// coarse-to-fine GNC x IRLS schedule.  Unity build: the kernel files are
+// included here so every kernel and its host launch live in one TU.
+//
+// The host never touches image data between kernels: one of_estimate_flow()
+// call uploads a pair, runs preprocessing, pyramids, every warping
+// iteration (warp, assembly, solve, update, occlusion, weighted median) on
+// one HIP stream, and downloads the flow.  The only host<->device syncs
+// inside a pair are the iterative solvers' convergence checks (one pinned
+// 80-byte read per chunk of iterations, double-buffered so the GPU always
+// has the next chunk queued) and Horn-Schunck's ||x|| < 1e-3 early exit.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "kernels_img.hip"
+#include "kernels_flow.hip"
+#include "kernels_solve.hip"
+
+namespace {
+
+struct OfError {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t e_ = (x);                                                                             \
+    if (e_ != hipSuccess) throw OfError{OF_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+#define REQUIRE(cond, code, msg) \
+  do {                           \
+    if (!(cond)) throw OfError{code, msg}; \
+  } while (0)
+
+// grow-only device arena: chunks are kept across calls, offsets reset per call
+struct Arena {
+  struct Chunk {
+    char *p;
+    size_t cap, off;
+  };
+  std::vector<Chunk> chunks;
+  void reset() {
+    for (auto &c : chunks) c.off = 0;
+  }
+  void *alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    for (auto &c : chunks)
+      if (c.cap - c.off >= bytes) {
+        void *r = c.p + c.off;
+        c.off += bytes;
+        return r;
+      }
+    size_t cap = bytes > ((size_t)64 << 20) ? bytes : ((size_t)64 << 20);
+    char *p = nullptr;
+    HIPCHK(hipMalloc(&p, cap));
+    chunks.push_back({p, cap, bytes});
+    return p;
+  }
+  void release() {
+    for (auto &c : chunks) hipFree(c.p);
+    chunks.clear();
+  }
+};
+
+struct Img {  // C planar pitched fp32 planes
+  float *p = nullptr;
+  int H = 0, W = 0, P = 0, C = 0;
+  size_t ps() const { return (size_t)H * P; }
+  float *plane(int c) const { return p + (size_t)c * ps(); }
+};
+struct F2 {  // pitched float2 field
+  float2 *p = nullptr;
+  int H = 0, W = 0, P = 0;
+};
+
+struct ProfRec {
+  const char *name;
+  hipEvent_t e0, e1;
+};
+
+struct Slot {
+  float *rgb1 = nullptr, *rgb2 = nullptr, *uv = nullptr;  // uv: dense planar 2 x H x W
+  int H = 0, W = 0, C = 0;
+  size_t cap_rgb = 0, cap_uv = 0;
+};
+
+}  // namespace
+
+struct of_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  Arena arena;
+  PcgState *d_state = nullptr, *h_state = nullptr;  // h_state: 2 pinned slots
+  hipEvent_t ev_state[2] = {nullptr, nullptr};
+  double *d_partials = nullptr;
+  unsigned *d_counter = nullptr;
+  uint32_t *d_mm = nullptr;  // 32 min/max pairs
+  double *d_norm = nullptr, *h_norm = nullptr;
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;  // profiling events
+  size_t ev_used = 0;
+  std::vector<hipEvent_t> tev_pool;  // level timing events, recycled per API call
+  size_t tev_used = 0;
+  std::vector<ProfRec> pending;
+  std::map<std::string, std::pair<double, int64_t>> ktimes;
+  std::vector<Slot> slots;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+constexpr int MAX_RED_BLOCKS = 2048;
+
+hipEvent_t pool_event(of_ctx *c) {
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[c->ev_used++];
+}
+
+hipEvent_t timing_event(of_ctx *c) {
+  if (c->tev_used == c->tev_pool.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->tev_pool.push_back(e);
+  }
+  return c->tev_pool[c->tev_used++];
+}
+
+void flush_prof(of_ctx *c) {
+  if (c->pending.empty()) return;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (auto &r : c->pending) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
+    auto &s = c->ktimes[r.name];
+    s.first += ms;
+    s.second += 1;
+  }
+  c->pending.clear();
+  c->ev_used = 0;
+}
+
+template <typename K, typename... A>
+void launch(of_ctx *c, const char *name, K kernel, dim3 g, dim3 b, size_t shm, A... args) {
+  if (g.x == 0 || g.y == 0 || g.z == 0) return;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof) {
+    if (c->ev_used + 2 > 8192) flush_prof(c);
+    e0 = pool_event(c);
+    e1 = pool_event(c);
+    HIPCHK(hipEventRecord(e0, c->stream));
+  }
+  hipLaunchKernelGGL(kernel, g, b, shm, c->stream, args...);
+  HIPCHK(hipGetLastError());
+  if (c->prof) {
+    HIPCHK(hipEventRecord(e1, c->stream));
+    c->pending.push_back({name, e0, e1});
+  }
+}
+
+inline dim3 gz(const Grid2 &g, int z) { return dim3(g.grid.x, g.grid.y, z); }
+
+Img new_img(of_ctx *c, int H, int W, int C) {
+  Img m;
+  m.H = H;
+  m.W = W;
+  m.C = C;
+  m.P = of_pitch(W);
+  m.p = (float *)c->arena.alloc(sizeof(float) * m.ps() * (C > 0 ? C : 1));
+  return m;
+}
+F2 new_f2(of_ctx *c, int H, int W) {
+  F2 f;
+  f.H = H;
+  f.W = W;
+  f.P = of_pitch(W);
+  f.p = (float2 *)c->arena.alloc(sizeof(float2) * (size_t)H * f.P);
+  return f;
+}
+Img view(const Img &m, int c0, int n) {
+  Img v = m;
+  v.p = m.plane(c0);
+  v.C = n;
+  return v;
+}
+
+// host planar dense (C x H x W) -> device pitched
+void upload_img(of_ctx *c, const Img &m, const float *host) {
+  HIPCHK(hipMemcpy2DAsync(m.p, sizeof(float) * m.P, host, sizeof(float) * m.W, sizeof(float) * m.W,
+                          (size_t)m.H * m.C, hipMemcpyHostToDevice, c->stream));
+}
+void download_img(of_ctx *c, const Img &m, float *host) {
+  HIPCHK(hipMemcpy2DAsync(host, sizeof(float) * m.W, m.p, sizeof(float) * m.P, sizeof(float) * m.W,
+                          (size_t)m.H * m.C, hipMemcpyDeviceToHost, c->stream));
+}
+void copy_img(of_ctx *c, const Img &dst, const Img &src) {
+  HIPCHK(hipMemcpyAsync(dst.p, src.p, sizeof(float) * src.ps() * src.C, hipMemcpyDeviceToDevice, c->stream));
+}
+// planar host/dense-device uv <-> pitched float2
+void f2_from_dense(of_ctx *c, const F2 &f, const float *dense_dev) {
+  Grid2 g = grid2(f.H, f.W);
+  launch(c, "planar2_to_f2", k_planar2_to_f2, g.grid, g.block, 0, dense_dev, f.p, f.H, f.W, f.P,
+         (size_t)f.H * f.W);
+}
+void f2_to_dense(of_ctx *c, const F2 &f, float *dense_dev) {
+  Grid2 g = grid2(f.H, f.W);
+  launch(c, "f2_to_planar2", k_f2_to_planar2, g.grid, g.block, 0, (const float2 *)f.p, dense_dev, f.H, f.W, f.P,
+         (size_t)f.H * f.W);
+}
+F2 upload_f2(of_ctx *c, const float *host, int H, int W) {
+  F2 f = new_f2(c, H, W);
+  float *d = (float *)c->arena.alloc(sizeof(float) * 2 * (size_t)H * W);
+  HIPCHK(hipMemcpyAsync(d, host, sizeof(float) * 2 * (size_t)H * W, hipMemcpyHostToDevice, c->stream));
+  f2_from_dense(c, f, d);
+  return f;
+}
+void download_f2(of_ctx *c, const F2 &f, float *host) {
+  float *d = (float *)c->arena.alloc(sizeof(float) * 2 * (size_t)f.H * f.W);
+  f2_to_dense(c, f, d);
+  HIPCHK(hipMemcpyAsync(host, d, sizeof(float) * 2 * (size_t)f.H * f.W, hipMemcpyDeviceToHost, c->stream));
+}
+void fill_f2(of_ctx *c, const F2 &f, float v) {
+  Grid2 g = grid2(f.H, f.W);
+  launch(c, "fill_f2", k_fill_f2, g.grid, g.block, 0, f.p, f.H, f.W, f.P, make_float2(v, v));
+}
+
+// ---- global scale_image over all planes of an image ------------------------
+void scale_img(of_ctx *c, const Img &m, float vlow, float vhigh, int mm_slot) {
+  uint32_t *mm = c->d_mm + 2 * mm_slot;
+  launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
+  Grid2 g = grid2(m.H, m.W);
+  launch(c, "minmax", k_minmax, g.grid, g.block, 0, (const float *)m.p, m.H, m.W, m.P, m.C, m.ps(), mm);
+  launch(c, "scale", k_scale, g.grid, g.block, 0, m.p, m.H, m.W, m.P, m.C, m.ps(), (const uint32_t *)mm, vlow, vhigh);
+}
+
+// ---- correlation taps -------------------------------------------------------
+Taps make_taps(const double *k, int kh, int kw) {
+  Taps t;
+  memset(&t, 0, sizeof(t));
+  t.kh = kh;
+  t.kw = kw;
+  for (int a = 0; a < kh * kw; ++a) t.w[a] = (float)k[a];
+  return t;
+}
+void correlate(of_ctx *c, const Img &in, const Img &out, const Taps &t) {
+  Grid2 g = grid2(in.H, in.W);
+  launch(c, "correlate", k_correlate, gz(g, in.C), g.block, 0, (const float *)in.p, out.p, in.H, in.W, in.P, in.ps(),
+         t);
+}
+
+// fspecial('gaussian') (image_processing.py:29-49)
+std::vector<double> gaussian(int size, double sigma) {
+  std::vector<double> k(size * size);
+  double m = (size - 1) / 2.0, mx = 0, s = 0;
+  for (int a = 0; a < size; ++a)
+    for (int b = 0; b < size; ++b) {
+      double y = a - m, x = b - m;
+      k[a * size + b] = std::exp(-(x * x + y * y) / (2 * sigma * sigma));
+      mx = std::max(mx, k[a * size + b]);
+    }
+  for (auto &v : k) {
+    if (v < 2.220446049250313e-16 * mx) v = 0;
+    s += v;
+  }
+  if (s != 0)
+    for (auto &v : k) v /= s;
+  return k;
+}
+
+void resize_dims(int H, int W, double ratio, int *nH, int *nW) {
+  int a = (int)std::floor(H * ratio + 0.5), b = (int)std::floor(W * ratio + 0.5);
+  *nH = a < 1 ? 1 : a;
+  *nW = b < 1 ? 1 : b;
+}
+
+// one compute_image_pyramid step (pyramid.py:58-67)
+Img pyramid_step(of_ctx *c, const Img &in, const Taps &t, double ratio) {
+  int nH, nW;
+  resize_dims(in.H, in.W, ratio, &nH, &nW);
+  Img tmp = new_img(c, in.H, in.W, in.C);
+  correlate(c, in, tmp, t);
+  Img out = new_img(c, nH, nW, in.C);
+  Grid2 g = grid2(nH, nW);
+  launch(c, "resize", k_resize<float>, gz(g, in.C), g.block, 0, (const float *)tmp.p, in.H, in.W, in.P, tmp.ps(),
+         out.p, nH, nW, out.P, out.ps(), 1.0f);
+  return out;
+}
+
+// _build_pyramid (base.py:174-190)
+std::vector<Img> build_pyramid(of_ctx *c, const Img &img, int levels, double spacing) {
+  double sig = std::sqrt(spacing) / std::sqrt(2.0);
+  int ks = 2 * (int)std::nearbyint(1.5 * sig) + 1;
+  auto k = gaussian(ks, sig);
+  Taps t = make_taps(k.data(), ks, ks);
+  std::vector<Img> pyr{img};
+  for (int l = 1; l < levels; ++l) pyr.push_back(pyramid_step(c, pyr.back(), t, 1.0 / spacing));
+  return pyr;
+}
+
+// structure_texture_decomposition_rof (image_processing.py:52-136) on all planes
+Img rof_texture(of_ctx *c, const Img &in, double theta, int iters, double alp) {
+  Img nrm = new_img(c, in.H, in.W, in.C);
+  copy_img(c, nrm, in);
+  scale_img(c, nrm, -1.0f, 1.0f, 0);
+  const size_t ps = nrm.ps();  // C planes of float2 p
+  float2 *p0 = (float2 *)c->arena.alloc(sizeof(float2) * ps * in.C);
+  float2 *p1 = (float2 *)c->arena.alloc(sizeof(float2) * ps * in.C);
+  HIPCHK(hipMemsetAsync(p0, 0, sizeof(float2) * ps * in.C, c->stream));
+  Grid2 g = grid2(in.H, in.W);
+  const float th = (float)theta, delta = (float)(1.0 / (4.0 * theta));
+  for (int it = 0; it < iters; ++it) {
+    launch(c, "rof_iter", k_rof_iter, gz(g, in.C), g.block, 0, (const float *)nrm.p, (const float2 *)p0, p1, in.H,
+           in.W, nrm.P, ps, th, delta);
+    std::swap(p0, p1);
+  }
+  Img out = new_img(c, in.H, in.W, in.C);
+  launch(c, "rof_final", k_rof_final, gz(g, in.C), g.block, 0, (const float *)nrm.p, (const float2 *)p0, out.p, in.H,
+         in.W, nrm.P, ps, th, (float)alp);
+  scale_img(c, out, 0.0f, 255.0f, 1);
+  return out;
+}
+
+// ---- per-level derivative planes ---------------------------------------------
+struct LevelDeriv {
+  Img I1x, I1y, A, B, Cc;
+  DerivArgs args;
+};
+
+LevelDeriv level_deriv(of_ctx *c, const Img &im, int nc, int interp, const double *filt, double blend) {
+  LevelDeriv L;
+  Img I1 = view(im, 0, nc), I2 = view(im, nc, nc);
+  Taps tx = make_taps(filt, 1, 5), ty = make_taps(filt, 5, 1);
+  L.I1x = new_img(c, im.H, im.W, nc);
+  L.I1y = new_img(c, im.H, im.W, nc);
+  correlate(c, I1, L.I1x, tx);
+  correlate(c, I1, L.I1y, ty);
+  L.A = new_img(c, im.H, im.W, nc);
+  L.B = new_img(c, im.H, im.W, nc);
+  L.Cc = new_img(c, im.H, im.W, nc);
+  correlate(c, I2, L.A, tx);
+  correlate(c, I2, L.B, ty);
+  if (interp == OF_INTERP_BICUBIC) {
+    double kxy[25];
+    for (int a = 0; a < 5; ++a)
+      for (int b = 0; b < 5; ++b) kxy[a * 5 + b] = filt[a] * filt[b];
+    correlate(c, I2, L.Cc, make_taps(kxy, 5, 5));
+  } else if (interp == OF_INTERP_CUBIC) {
+    // B-spline coefficients of I2x, I2y (in place via tmp) and of I2 (into Cc)
+    BsplTaps bt;
+    const double z = std::sqrt(3.0) - 2.0, c0 = -6.0 * z / (1.0 - z * z);
+    for (int k = 0; k <= OF_BSPL_K; ++k) bt.h[k] = (float)(c0 * std::pow(z, (double)k));
+    Img tmp = new_img(c, im.H, im.W, nc);
+    Grid2 g = grid2(im.H, im.W);
+    auto pf = [&](const Img &src, const Img &dst) {
+      launch(c, "bspline_rows", k_bspline_rows, gz(g, nc), g.block, 0, (const float *)src.p, tmp.p, im.H, im.W, im.P,
+             im.ps(), bt);
+      launch(c, "bspline_cols", k_bspline_cols, gz(g, nc), g.block, 0, (const float *)tmp.p, dst.p, im.H, im.W, im.P,
+             im.ps(), bt);
+    };
+    pf(L.A, L.A);
+    pf(L.B, L.B);
+    pf(I2, L.Cc);
+  }
+  DerivArgs &d = L.args;
+  d.I1 = I1.p;
+  d.I2 = I2.p;
+  d.I1x = L.I1x.p;
+  d.I1y = L.I1y.p;
+  d.A = L.A.p;
+  d.B = L.B.p;
+  d.Cc = L.Cc.p;
+  d.nc = nc;
+  d.blend = (float)blend;
+  return L;
+}
+
+void partial_deriv(of_ctx *c, const LevelDeriv &L, int interp, const F2 &uv, const Img &It, const Img &Ix,
+                   const Img &Iy) {
+  Grid2 g = grid2(uv.H, uv.W);
+  const size_t ps = It.ps();
+  if (interp == OF_INTERP_BICUBIC)
+    launch(c, "partial_deriv_hermite", k_partial_deriv<1>, g.grid, g.block, 0, L.args, (const float2 *)uv.p, uv.H,
+           uv.W, uv.P, ps, It.p, Ix.p, Iy.p);
+  else if (interp == OF_INTERP_CUBIC)
+    launch(c, "partial_deriv_bspline", k_partial_deriv<0>, g.grid, g.block, 0, L.args, (const float2 *)uv.p, uv.H,
+           uv.W, uv.P, ps, It.p, Ix.p, Iy.p);
+  else
+    launch(c, "partial_deriv_bilinear", k_partial_deriv<2>, g.grid, g.block, 0, L.args, (const float2 *)uv.p, uv.H,
+           uv.W, uv.P, ps, It.p, Ix.p, Iy.p);
+}
+
+OpArgs op_args(const of_params *P, double alpha, double lambda2) {
+  OpArgs o;
+  memset(&o, 0, sizeof(o));
+  o.qd = to_penf(P->qua_data);
+  o.rd = to_penf(P->rho_data);
+  for (int k = 0; k < 2; ++k) {
+    o.qsu[k] = to_penf(P->qua_spatial_u[k]);
+    o.qsv[k] = to_penf(P->qua_spatial_v[k]);
+    o.rsu[k] = to_penf(P->rho_spatial_u[k]);
+    o.rsv[k] = to_penf(P->rho_spatial_v[k]);
+  }
+  o.rc = to_penf(P->rho_couple);
+  // alpha == 1: quadratic system only; alpha == 0: robust only; else blend
+  // (classic_nl.py:237-248, ba.py:374-385)
+  o.use_q = alpha > 0.0;
+  o.use_r = alpha < 1.0;
+  o.aq_s = (float)((o.use_r ? alpha : 1.0) * P->lambda_q);
+  o.ar_s = (float)((o.use_q ? 1.0 - alpha : 1.0) * P->lambda_);
+  o.aq_d = (float)(o.use_r ? alpha : 1.0);
+  o.ar_d = (float)(o.use_q ? 1.0 - alpha : 1.0);
+  o.lambda2 = (float)lambda2;
+  return o;
+}
+
+void flow_operator(of_ctx *c, const OpArgs &o, const F2 &uv, const F2 *duv, const Img &It, const Img &Ix,
+                   const Img &Iy, const F2 *uvhat, const Img &coef, const F2 &rhs) {
+  Grid2 g = grid2(uv.H, uv.W);
+  launch(c, "flow_operator", k_flow_operator, g.grid, g.block, 0, o, (const float2 *)uv.p,
+         (const float2 *)(duv ? duv->p : nullptr), (const float *)It.p, (const float *)Ix.p, (const float *)Iy.p, It.C,
+         (const float2 *)(uvhat ? uvhat->p : nullptr), uv.H, uv.W, uv.P, coef.ps(), coef.p, rhs.p);
+}
+
+// ---- iterative solve (base.py:87-172) -----------------------------------------
+struct SolveResult {
+  int iters;
+  int done;
+  double rel;
+};
+
+SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+  const int H = b.H, W = b.W;
+  Grid2 g = grid2(H, W, MAX_RED_BLOCKS);
+  const size_t ps = coef.ps();
+  const int solver = P->solver;
+  int maxiter;
+  if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
+    const bool block = solver == OF_SOLVER_BACKSLASH;
+    const double rtol = block ? P->exact_rtol : P->pcg_rtol;
+    maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
+    F2 r = new_f2(c, H, W), z = new_f2(c, H, W), pa = new_f2(c, H, W), pb = new_f2(c, H, W), q = new_f2(c, H, W);
+    if (block)
+      launch(c, "pcg_init", k_pcg_init<true>, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p,
+             r.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter, rtol, maxiter);
+    else
+      launch(c, "pcg_init", k_pcg_init<false>, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p,
+             r.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter, rtol, maxiter);
+    int enq = 0, chunk = 8, nchunks = 0;
+    F2 pold = pa, pnew = pb;
+    while (true) {
+      int n = std::min(chunk, maxiter - enq);
+      for (int t = 0; t < n; ++t) {
+        launch(c, "pcg_spmv", k_pcg_dir_spmv, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)z.p,
+               (const float2 *)pold.p, pnew.p, q.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter);
+        if (block)
+          launch(c, "pcg_update", k_pcg_update<true>, g.grid, g.block, 0, (const float *)coef.p, x.p, r.p,
+                 (const float2 *)pnew.p, (const float2 *)q.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials,
+                 c->d_counter);
+        else
+          launch(c, "pcg_update", k_pcg_update<false>, g.grid, g.block, 0, (const float *)coef.p, x.p, r.p,
+                 (const float2 *)pnew.p, (const float2 *)q.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials,
+                 c->d_counter);
+        std::swap(pold, pnew);
+      }
+      enq += n;
+      const int slot = nchunks & 1;
+      HIPCHK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipEventRecord(c->ev_state[slot], c->stream));
+      ++nchunks;
+      if (enq >= maxiter) break;
+      if (nchunks >= 2) {  // check the previous chunk while this one runs
+        HIPCHK(hipEventSynchronize(c->ev_state[slot ^ 1]));
+        if (c->h_state[slot ^ 1].done) break;
+      }
+      chunk = std::min(chunk * 2, 64);
+    }
+    HIPCHK(hipEventSynchronize(c->ev_state[(nchunks - 1) & 1]));
+    const PcgState &s = c->h_state[(nchunks - 1) & 1];
+    return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
+  }
+  // red-black block SOR
+  maxiter = P->sor_max_iters;
+  launch(c, "sor_init", k_sor_init, g.grid, g.block, 0, x.p, H, W, b.P, c->d_state, maxiter);
+  int enq = 0, chunk = 16, nchunks = 0;
+  while (true) {
+    int n = std::min(chunk, maxiter - enq);
+    for (int t = 0; t < n; ++t)
+      for (int color = 0; color < 2; ++color)
+        launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p, H, W,
+               b.P, ps, color, (float)P->sor_omega, (float)P->sor_tol, c->d_state, c->d_partials, c->d_counter);
+    enq += n;
+    const int slot = nchunks & 1;
+    HIPCHK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(c->ev_state[slot], c->stream));
+    ++nchunks;
+    if (enq >= maxiter) break;
+    if (nchunks >= 2) {
+      HIPCHK(hipEventSynchronize(c->ev_state[slot ^ 1]));
+      if (c->h_state[slot ^ 1].done) break;
+    }
+    chunk = std::min(chunk * 2, 128);
+  }
+  HIPCHK(hipEventSynchronize(c->ev_state[(nchunks - 1) & 1]));
+  const PcgState &s = c->h_state[(nchunks - 1) & 1];
+  return {s.iter, s.done, 0.0};
+}
+
+void note_solve(of_stats *st, const SolveResult &r) {
+  if (!st) return;
+  st->solves++;
+  st->solver_iters_total += r.iters;
+  st->solver_iters_max = std::max(st->solver_iters_max, r.iters);
+  if (r.done == 2) st->solves_not_converged++;
+}
+
+double norm2(of_ctx *c, const F2 &x) {
+  Grid2 g = grid2(x.H, x.W, MAX_RED_BLOCKS);
+  launch(c, "norm2", k_norm2, g.grid, g.block, 0, (const float2 *)x.p, x.H, x.W, x.P, c->d_partials, c->d_counter,
+         c->d_norm);
+  HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return *c->h_norm;
+}
+
+void median2(of_ctx *c, const F2 &in, const F2 &out, int size) {
+  Grid2 g = grid2(in.H, in.W);
+  if (size == 5)
+    launch(c, "median5", k_median2<5>, g.grid, g.block, 0, (const float2 *)in.p, out.p, in.H, in.W, in.P);
+  else if (size == 3)
+    launch(c, "median3", k_median2<3>, g.grid, g.block, 0, (const float2 *)in.p, out.p, in.H, in.W, in.P);
+  else if (size == 7)
+    launch(c, "median7", k_median2<7>, g.grid, g.block, 0, (const float2 *)in.p, out.p, in.H, in.W, in.P);
+  else
+    throw OfError{OF_ENOTSUP, "median_filter_size must be 3, 5 or 7"};
+}
+
+void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &out, int hsz, double sigma_i) {
+  REQUIRE(guide.C == 1 || guide.C == 3, OF_ENOTSUP, "weighted median guide must have 1 or 3 channels");
+  REQUIRE(hsz >= 0 && hsz <= 12, OF_ENOTSUP, "area_hsz must be <= 12");
+  const int RW = WMF_T + 2 * hsz, nreg = RW * RW;
+  int npow2 = 1;
+  while (npow2 < nreg) npow2 <<= 1;
+  const size_t shm = 2 * (size_t)npow2 * sizeof(uint64_t) + (size_t)(guide.C + 1) * nreg * sizeof(float);
+  dim3 grid((uv.W + WMF_T - 1) / WMF_T, (uv.H + WMF_T - 1) / WMF_T);
+  const float inv = (float)(1.0 / (2.0 * sigma_i * sigma_i));
+  if (guide.C == 3)
+    launch(c, "wmf", k_wmf<3>, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H,
+           uv.W, uv.P, guide.ps(), hsz, inv, RW, nreg, npow2);
+  else
+    launch(c, "wmf", k_wmf<1>, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H,
+           uv.W, uv.P, guide.ps(), hsz, inv, RW, nreg, npow2);
+}
+
+void resample_f2(of_ctx *c, const F2 &in, const F2 &out) {
+  const float ratio = (float)((double)out.H / (double)in.H);
+  Grid2 g = grid2(out.H, out.W);
+  launch(c, "resample_flow", k_resize<float2>, g.grid, g.block, 0, (const float2 *)in.p, in.H, in.W, in.P,
+         (size_t)in.H * in.P, out.p, out.H, out.W, out.P, (size_t)out.H * out.P, ratio);
+}
+
+// ---- the per-level IRLS loops ----------------------------------------------
+struct LevelIn {
+  Img im;     // 2*nc planes
+  Img guide;  // gc planes or p == nullptr
+};
+
+// HSOpticalFlow.compute_flow_base (hs.py:109-142)
+void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
+  const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, 0.5);
+  Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
+  Img coef = new_img(c, H, W, 7);
+  F2 rhs = new_f2(c, H, W), x = new_f2(c, H, W), tmp = new_f2(c, H, W);
+  OpArgs o = op_args(P, 0.0, 0.0);
+  Grid2 g = grid2(H, W);
+  for (int it = 0; it < P->max_warping_iters; ++it) {
+    partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
+    flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
+    note_solve(st, solve(c, P, coef, rhs, x));
+    if (std::sqrt(norm2(c, x)) < 1e-3) break;
+    launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)x.p, P->limit_update, H, W, uv.P);
+    if (P->median_filter_size)
+      for (int m = 0; m < P->mf_iter; ++m) {
+        median2(c, uv, tmp, P->median_filter_size);
+        std::swap(uv.p, tmp.p);
+      }
+  }
+}
+
+// BAOpticalFlow / ClassicNLOpticalFlow compute_flow_base (ba.py:143-206,
+// classic_nl.py:200-277)
+void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double alpha, int max_linear,
+               of_stats *st) {
+  const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  const double blend = P->method == OF_METHOD_BA ? P->blend : 0.5;  // classic_nl.py:232 passes no blend
+  LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, blend);
+  Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
+  Img coef = new_img(c, H, W, 7);
+  Img occ = new_img(c, H, W, 1);
+  F2 rhs = new_f2(c, H, W), x = new_f2(c, H, W), uv1 = new_f2(c, H, W), uv2 = new_f2(c, H, W);
+  F2 duv = new_f2(c, H, W);
+  OpArgs o = op_args(P, alpha, 0.0);
+  Grid2 g = grid2(H, W);
+  const bool nl = P->method == OF_METHOD_CLASSIC_NL;
+  for (int it = 0; it < P->max_iters; ++it) {
+    partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
+    for (int jl = 0; jl < max_linear; ++jl) {
+      flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
+      note_solve(st, solve(c, P, coef, rhs, x));
+      const bool filt = P->median_filter_size != 0;
+      launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
+             (const float2 *)uv.p, (const float2 *)x.p, P->limit_update, uv1.p, (const float *)L.im.p,
+             (const float *)L.im.plane(nc), nc, (nl && filt && L.guide.p) ? occ.p : (float *)nullptr, H, W, uv.P,
+             L.im.ps());
+      F2 res = uv1;
+      if (filt) {
+        if (nl && L.guide.p) wmf(c, uv1, L.guide, occ.p, uv2, P->area_hsz, P->sigma_i);
+        else median2(c, uv1, uv2, P->median_filter_size);
+        res = uv2;
+      }
+      if (jl + 1 < max_linear)  // duv = filtered - uv feeds the next linearisation
+        launch(c, "sub2", k_sub2, g.grid, g.block, 0, (const float2 *)uv.p, (const float2 *)res.p, duv.p, H, W, uv.P);
+      else  // uv = uv0 + (filtered - uv0)  (classic_nl.py:271-275, ba.py:404-407)
+        launch(c, "axpy_diff", k_axpy_diff, g.grid, g.block, 0, uv.p, (const float2 *)uv.p, (const float2 *)res.p, H,
+               W, uv.P);
+    }
+  }
+}
+
+// AltBAOpticalFlow.compute_flow_base (alt_ba.py:189-274)
+void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvhat, double alpha, bool replacement,
+                of_stats *st) {
+  const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, 0.5);
+  Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
+  Img coef = new_img(c, H, W, 7);
+  F2 rhs = new_f2(c, H, W), x = new_f2(c, H, W), duv = new_f2(c, H, W), t1 = new_f2(c, H, W), t2 = new_f2(c, H, W);
+  Grid2 g = grid2(H, W);
+  const int n = P->max_iters;
+  std::vector<double> l2s(n + 1);
+  const double a = std::log10(1e-4), b = std::log10(P->lambda2);
+  for (int t = 0; t < n; ++t) l2s[t] = std::pow(10.0, n == 1 ? a : a + (b - a) * t / (n - 1));
+  l2s[n] = P->lambda2;
+  double lambda2 = l2s[0];
+  for (int i = 0; i < n; ++i) {
+    partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
+    OpArgs o = op_args(P, alpha, lambda2);
+    bool have_duv = false;
+    for (int jl = 0; jl < P->max_linear; ++jl) {
+      flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
+      note_solve(st, solve(c, P, coef, rhs, x));
+      // duv = clip(x): computed as (0 + clip(x))
+      HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
+      launch(c, "add_update", k_add_update, g.grid, g.block, 0, duv.p, (const float2 *)x.p, P->limit_update, H, W,
+             duv.P);
+      have_duv = true;
+    }
+    if (have_duv)
+      launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)duv.p, 0, H, W, uv.P);
+    // uvhat = denoise_LO(uv) per component (denoising.py:6-30)
+    if (P->median_filter_size) {
+      HIPCHK(hipMemcpyAsync(t1.p, uv.p, sizeof(float2) * (size_t)H * uv.P, hipMemcpyDeviceToDevice, c->stream));
+      const float lam = (float)(lambda2 / P->lambda3);
+      for (int k = 0; k < P->itersLO; ++k) {
+        launch(c, "lo_blend", k_lo_blend, g.grid, g.block, 0, (const float2 *)t1.p, (const float2 *)uv.p, lam, t2.p, H,
+               W, uv.P);
+        median2(c, t2, t1, P->median_filter_size);
+      }
+      HIPCHK(hipMemcpyAsync(uvhat.p, t1.p, sizeof(float2) * (size_t)H * uv.P, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      HIPCHK(hipMemcpyAsync(uvhat.p, uv.p, sizeof(float2) * (size_t)H * uv.P, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (replacement)
+      HIPCHK(hipMemcpyAsync(uv.p, uvhat.p, sizeof(float2) * (size_t)H * uv.P, hipMemcpyDeviceToDevice, c->stream));
+    lambda2 = l2s[i + 1];
+  }
+}
+
+int auto_levels(int H, int W, double spacing) {
+  int m = H < W ? H : W;  // base.py:192-195
+  return 1 + (int)std::floor(std::log(m / 16.0) / std::log(spacing));
+}
+
+void check_params(const of_params *P) {
+  REQUIRE(P->method >= 0 && P->method <= 3, OF_EINVAL, "unknown method");
+  REQUIRE(P->solver >= 0 && P->solver <= 2, OF_EINVAL, "Unknown solver");
+  REQUIRE(P->interp >= 0 && P->interp <= 2, OF_EINVAL, "Unknown interpolation method");
+  REQUIRE(P->median_filter_size == 0 || P->median_filter_size == 3 || P->median_filter_size == 5 ||
+              P->median_filter_size == 7,
+          OF_ENOTSUP, "median_filter_size must be None, 3, 5 or 7");
+}
+
+// compute_flow (hs.py:49-99, ba.py:57-138, classic_nl.py:89-198, alt_ba.py:81-187)
+// images: device 2nc planes; guide: device gc planes or p == nullptr;
+// uv_io: full-resolution flow (init in, result out).
+void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &guide, F2 &uv_io, of_stats *st) {
+  check_params(P);
+  const int H = images.H, W = images.W, C = images.C, nc = C / 2;
+  REQUIRE(nc >= 1 && nc <= OF_MAX_NC, OF_ENOTSUP, "1..4 channels per frame supported");
+  hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
+  HIPCHK(hipEventRecord(t0, c->stream));
+  // preprocessing
+  Img img;
+  if (P->texture) {
+    const double alp = (P->method == OF_METHOD_HS || P->method == OF_METHOD_ALT_BA) ? 0.95 : P->alp;
+    img = rof_texture(c, images, 1.0 / 8, 100, alp);
+  } else if (P->fc && (P->method == OF_METHOD_BA || P->method == OF_METHOD_CLASSIC_NL)) {
+    // images - alp * correlate(images, gaussian(5, 1.5)) then [0, 255]
+    // (classic_nl.py:109-113, ba.py:280-285), per channel
+    auto gk = gaussian(5, 1.5);
+    Img sm = new_img(c, H, W, C);
+    correlate(c, images, sm, make_taps(gk.data(), 5, 5));
+    img = new_img(c, H, W, C);
+    Grid2 g = grid2(H, W);
+    launch(c, "sub_scaled", k_sub_scaled, gz(g, C), g.block, 0, (const float *)images.p, (const float *)sm.p,
+           (float)P->alp, img.p, H, W, img.P, img.ps());
+    scale_img(c, img, 0.0f, 255.0f, 2);
+  } else {
+    img = new_img(c, H, W, C);
+    copy_img(c, img, images);
+    scale_img(c, img, 0.0f, 255.0f, 2);
+  }
+  int levels = P->pyramid_levels;
+  if (P->method == OF_METHOD_HS || P->method == OF_METHOD_ALT_BA || P->auto_level)
+    levels = auto_levels(H, W, P->pyramid_spacing);
+  P->pyramid_levels = levels;
+  REQUIRE(levels <= OF_MAX_LEVELS, OF_EINVAL, "too many pyramid levels");
+  std::vector<Img> pyr = build_pyramid(c, img, levels, P->pyramid_spacing), gpyr, cpyr, cgpyr;
+  if (P->method != OF_METHOD_HS) gpyr = build_pyramid(c, img, P->gnc_pyramid_levels, P->gnc_pyramid_spacing);
+  const bool use_guide = P->method == OF_METHOD_CLASSIC_NL && guide.p;
+  if (use_guide) {
+    cpyr = build_pyramid(c, guide, levels, P->pyramid_spacing);
+    cgpyr = build_pyramid(c, guide, P->gnc_pyramid_levels, P->gnc_pyramid_spacing);
+  }
+  HIPCHK(hipEventRecord(t1, c->stream));
+  F2 uv = uv_io, uvhat;
+  if (P->method == OF_METHOD_ALT_BA) {
+    uvhat = new_f2(c, H, W);
+    HIPCHK(hipMemcpyAsync(uvhat.p, uv.p, sizeof(float2) * (size_t)H * uv.P, hipMemcpyDeviceToDevice, c->stream));
+  }
+  const double alpha_orig = P->alpha;
+  const int gnc = P->method == OF_METHOD_HS ? 1 : P->gnc_iters;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> lev_ev;
+  for (int ig = 0; ig < gnc; ++ig) {
+    const int nl = ig == 0 ? levels : P->gnc_pyramid_levels;
+    const std::vector<Img> &lv = ig == 0 ? pyr : gpyr;
+    for (int l = nl - 1; l >= 0; --l) {
+      const int h = lv[l].H, w = lv[l].W;
+      hipEvent_t e0 = timing_event(c), e1 = timing_event(c);
+      HIPCHK(hipEventRecord(e0, c->stream));
+      if (uv.H != h || uv.W != w) {
+        F2 nuv = new_f2(c, h, w);
+        resample_f2(c, uv, nuv);
+        uv = nuv;
+        if (uvhat.p) {
+          F2 nh = new_f2(c, h, w);
+          resample_f2(c, uvhat, nh);
+          uvhat = nh;
+        }
+      }
+      LevelIn L;
+      L.im = lv[l];
+      if (use_guide) L.guide = (ig == 0 ? cpyr : cgpyr)[l];
+      if (P->method == OF_METHOD_HS) hs_base(c, P, L, uv, st);
+      else if (P->method == OF_METHOD_ALT_BA) altba_base(c, P, L, uv, uvhat, P->alpha, ig != gnc - 1, st);
+      else irls_base(c, P, L, uv, P->alpha, ig == 0 ? 1 : P->max_linear, st);
+      HIPCHK(hipEventRecord(e1, c->stream));
+      if (st && st->n_levels < OF_MAX_LEVELS) {
+        st->level_h[st->n_levels] = h;
+        st->level_w[st->n_levels] = w;
+        st->level_stage[st->n_levels] = ig;
+        st->n_levels++;
+        lev_ev.push_back({e0, e1});
+      }
+    }
+    if (gnc > 1) {  // GNC alpha schedule (classic_nl.py:180-184, ba.py:329-333)
+      const double na = 1.0 - (ig + 1.0) / (gnc - 1.0);
+      P->alpha = std::max(0.0, std::min(P->alpha, na));
+    }
+  }
+  if (P->method == OF_METHOD_BA) P->alpha = alpha_orig;  // ba.py:338-339
+  if (P->method == OF_METHOD_HS && P->median_filter_size && uv.H == H && uv.W == W) {  // hs.py:94-97
+    F2 t = new_f2(c, H, W);
+    median2(c, uv, t, P->median_filter_size);
+    uv = t;
+  }
+  const F2 &res = P->method == OF_METHOD_ALT_BA && uvhat.H == H ? uvhat : uv;
+  if (res.H == H && res.W == W && res.p != uv_io.p)
+    HIPCHK(hipMemcpyAsync(uv_io.p, res.p, sizeof(float2) * (size_t)H * uv_io.P, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, t0, t1));
+    st->preprocess_ms += ms;
+    for (size_t k = 0; k < lev_ev.size(); ++k) {
+      HIPCHK(hipEventElapsedTime(&ms, lev_ev[k].first, lev_ev[k].second));
+      st->level_ms[k] = ms;
+    }
+  }
+}
+
+// estimate_flow preprocessing (interface.py:41-64): host or device RGB input
+void estimate_dev(of_ctx *c, of_params *P, const float *rgb1, const float *rgb2, int H, int W, int C, F2 &uv,
+                  of_stats *st) {
+  REQUIRE(C == 1 || C == 3, OF_EINVAL, "images must be (H,W) or (H,W,3)");
+  hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
+  HIPCHK(hipEventRecord(t0, c->stream));
+  Img gray = new_img(c, H, W, 2);
+  const bool guide_mode = P->guide_mode && P->method == OF_METHOD_CLASSIC_NL;
+  Img guide;
+  if (guide_mode) guide = new_img(c, H, W, C == 3 ? 3 : 1);
+  uint32_t *mm = c->d_mm + 2 * 8;
+  launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
+  if (C == 3) {
+    const long n = (long)H * W * 3;
+    launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, rgb1, n, mm);
+  }
+  Grid2 g = grid2(H, W);
+  launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, rgb1, rgb2, H, W, C, gray.p, gray.P, gray.ps(),
+         guide_mode ? guide.p : (float *)nullptr, (const uint32_t *)mm);
+  if (guide_mode && C == 3)
+    for (int ch = 0; ch < 3; ++ch) scale_img(c, view(guide, ch, 1), 0.0f, 255.0f, 9 + ch);
+  HIPCHK(hipEventRecord(t1, c->stream));
+  compute_flow_dev(c, P, gray, guide, uv, st);
+  if (st) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, t0, t1));
+    st->preprocess_ms += ms;
+  }
+}
+
+int fail(of_ctx *c, const OfError &e) {
+  if (c) c->err = e.msg;
+  return e.code;
+}
+
+thread_local std::string g_err;
+
+}  // namespace
+
+#define API_BEGIN(ctx)            \
+  if (!ctx) return OF_EINVAL;     \
+  try {                           \
+    HIPCHK(hipSetDevice(ctx->device)); \
+    ctx->arena.reset();            \
+    ctx->tev_used = 0;
+#define API_END(ctx)                         \
+  flush_prof(ctx);                           \
+  return OF_OK;                              \
+  }                                          \
+  catch (const OfError &e) {                 \
+    ctx->pending.clear();                    \
+    ctx->ev_used = 0;                        \
+    return fail(ctx, e);                     \
+  }                                          \
+  catch (const std::exception &e) {          \
+    return fail(ctx, OfError{OF_ENOMEM, e.what()}); \
+  }
+
+extern "C" {
+
+int of_abi_version(void) { return OF_ABI_VERSION; }
+
+int of_device_count(int *count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  if (count) *count = n;
+  return OF_OK;
+}
+
+int of_ctx_create(int device, of_ctx **out) {
+  if (!out) return OF_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    g_err = "no HIP device";
+    return OF_EHIP;
+  }
+  of_ctx *c = new of_ctx();
+  c->device = device;
+  try {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->d_state, sizeof(PcgState)));
+    HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
+    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 4 * MAX_RED_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_counter, sizeof(unsigned) * 16));
+    HIPCHK(hipMemset(c->d_counter, 0, sizeof(unsigned) * 16));
+    HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
+    HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
+    HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));
+  } catch (const OfError &e) {
+    g_err = e.msg;
+    delete c;
+    return e.code;
+  }
+  *out = c;
+  return OF_OK;
+}
+
+int of_ctx_destroy(of_ctx *c) {
+  if (!c) return OF_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->arena.release();
+  for (auto &s : c->slots) {
+    hipFree(s.rgb1);
+    hipFree(s.rgb2);
+    hipFree(s.uv);
+  }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (auto e : c->tev_pool) hipEventDestroy(e);
+  for (auto e : c->ev_state)
+    if (e) hipEventDestroy(e);
+  hipFree(c->d_state);
+  hipHostFree(c->h_state);
+  hipFree(c->d_partials);
+  hipFree(c->d_counter);
+  hipFree(c->d_mm);
+  hipFree(c->d_norm);
+  hipHostFree(c->h_norm);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return OF_OK;
+}
+
+const char *of_last_error(of_ctx *c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int of_synchronize(of_ctx *c) {
+  if (!c) return OF_EINVAL;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? OF_OK : OF_EHIP;
+}
+
+int of_set_profiling(of_ctx *c, int enable) {
+  if (!c) return OF_EINVAL;
+  try {
+    flush_prof(c);
+  } catch (const OfError &e) {
+    return fail(c, e);
+  }
+  c->prof = enable != 0;
+  if (enable) c->ktimes.clear();
+  return OF_OK;
+}
+
+int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t *count, int *n) {
+  if (!c || !n) return OF_EINVAL;
+  int k = 0;
+  for (auto &kv : c->ktimes) {
+    if (k < max) {
+      if (names) names[k] = kv.first.c_str();
+      if (ms) ms[k] = kv.second.first;
+      if (count) count[k] = kv.second.second;
+    }
+    ++k;
+  }
+  *n = k;
+  return OF_OK;
+}
+
+int of_estimate_flow(of_ctx *c, of_params *P, const float *im1, const float *im2, int H, int W, int C,
+                     const float *init_uv, float *out_uv, of_stats *st) {
+  API_BEGIN(c)
+  REQUIRE(P && im1 && im2 && out_uv && H > 0 && W > 0, OF_EINVAL, "bad arguments");
+  if (st) memset(st, 0, sizeof(*st));
+  auto wall0 = std::chrono::steady_clock::now();
+  const size_t n = (size_t)H * W * C;
+  float *d1 = (float *)c->arena.alloc(sizeof(float) * n), *d2 = (float *)c->arena.alloc(sizeof(float) * n);
+  HIPCHK(hipMemcpyAsync(d1, im1, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d2, im2, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  F2 uv = init_uv ? upload_f2(c, init_uv, H, W) : new_f2(c, H, W);
+  if (!init_uv) fill_f2(c, uv, 0.0f);
+  estimate_dev(c, P, d1, d2, H, W, C, uv, st);
+  download_f2(c, uv, out_uv);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st)
+    st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  API_END(c)
+}
+
+int of_compute_flow(of_ctx *c, of_params *P, const float *images, int H, int W, int nc, const float *guide, int gc,
+                    const float *init_uv, float *out_uv, of_stats *st) {
+  API_BEGIN(c)
+  REQUIRE(P && images && out_uv && H > 0 && W > 0 && nc >= 1, OF_EINVAL, "bad arguments");
+  if (st) memset(st, 0, sizeof(*st));
+  auto wall0 = std::chrono::steady_clock::now();
+  Img im = new_img(c, H, W, 2 * nc);
+  upload_img(c, im, images);
+  Img g;
+  if (guide && gc > 0) {
+    g = new_img(c, H, W, gc);
+    upload_img(c, g, guide);
+  }
+  F2 uv = init_uv ? upload_f2(c, init_uv, H, W) : new_f2(c, H, W);
+  if (!init_uv) fill_f2(c, uv, 0.0f);
+  compute_flow_dev(c, P, im, g, uv, st);
+  download_f2(c, uv, out_uv);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st)
+    st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  API_END(c)
+}
+
+int of_compute_flow_base(of_ctx *c, of_params *P, const float *images, int H, int W, int nc, const float *guide,
+                         int gc, double alpha, const float *uv_in, float *out_uv) {
+  API_BEGIN(c)
+  REQUIRE(P && images && uv_in && out_uv, OF_EINVAL, "bad arguments");
+  check_params(P);
+  Img im = new_img(c, H, W, 2 * nc);
+  upload_img(c, im, images);
+  LevelIn L;
+  L.im = im;
+  if (guide && gc > 0 && P->method == OF_METHOD_CLASSIC_NL) {
+    L.guide = new_img(c, H, W, gc);
+    upload_img(c, L.guide, guide);
+  }
+  F2 uv = upload_f2(c, uv_in, H, W);
+  if (P->method == OF_METHOD_HS) hs_base(c, P, L, uv, nullptr);
+  else if (P->method == OF_METHOD_ALT_BA) throw OfError{OF_ENOTSUP, "AltBA compute_flow_base needs uvhat"};
+  else irls_base(c, P, L, uv, alpha, P->max_linear, nullptr);
+  download_f2(c, uv, out_uv);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+// ---- device-resident slots ----
+int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int H, int W, int C) {
+  API_BEGIN(c)
+  REQUIRE(slot >= 0 && slot < 4096 && im1 && im2 && (C == 1 || C == 3), OF_EINVAL, "bad arguments");
+  if ((int)c->slots.size() <= slot) c->slots.resize(slot + 1);
+  Slot &s = c->slots[slot];
+  const size_t n = (size_t)H * W * C, nu = 2 * (size_t)H * W;
+  if (s.cap_rgb < n) {
+    hipFree(s.rgb1);
+    hipFree(s.rgb2);
+    HIPCHK(hipMalloc(&s.rgb1, sizeof(float) * n));
+    HIPCHK(hipMalloc(&s.rgb2, sizeof(float) * n));
+    s.cap_rgb = n;
+  }
+  if (s.cap_uv < nu) {
+    hipFree(s.uv);
+    HIPCHK(hipMalloc(&s.uv, sizeof(float) * nu));
+    s.cap_uv = nu;
+  }
+  s.H = H;
+  s.W = W;
+  s.C = C;
+  HIPCHK(hipMemcpyAsync(s.rgb1, im1, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(s.rgb2, im2, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_pair_run(of_ctx *c, int slot, of_params *P, of_stats *st) {
+  API_BEGIN(c)
+  REQUIRE(slot >= 0 && slot < (int)c->slots.size() && c->slots[slot].rgb1, OF_EINVAL, "slot not uploaded");
+  Slot &s = c->slots[slot];
+  if (st) memset(st, 0, sizeof(*st));
+  auto wall0 = std::chrono::steady_clock::now();
+  F2 uv = new_f2(c, s.H, s.W);
+  fill_f2(c, uv, 0.0f);
+  estimate_dev(c, P, s.rgb1, s.rgb2, s.H, s.W, s.C, uv, st);
+  f2_to_dense(c, uv, s.uv);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st)
+    st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  API_END(c)
+}
+
+int of_pair_download(of_ctx *c, int slot, float *out_uv) {
+  API_BEGIN(c)
+  REQUIRE(slot >= 0 && slot < (int)c->slots.size() && c->slots[slot].uv && out_uv, OF_EINVAL, "bad slot");
+  Slot &s = c->slots[slot];
+  HIPCHK(hipMemcpyAsync(out_uv, s.uv, sizeof(float) * 2 * (size_t)s.H * s.W, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+// ---- RCCL gather: one process per GPU ----
+int of_rccl_unique_id(char *out128) {
+  if (!out128) return OF_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return OF_ERCCL;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(out128, &id, 128);
+  return OF_OK;
+}
+
+int of_rccl_init(of_ctx *c, const char *id128, int nranks, int rank) {
+  API_BEGIN(c)
+  REQUIRE(id128 && nranks >= 1 && rank >= 0 && rank < nranks, OF_EINVAL, "bad arguments");
+  ncclUniqueId id;
+  memcpy(&id, id128, 128);
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  REQUIRE(r == ncclSuccess, OF_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  c->nranks = nranks;
+  c->rank = rank;
+  API_END(c)
+}
+
+int of_rccl_gather_flows(of_ctx *c, int nslots, float *out_uv_rank0) {
+  API_BEGIN(c)
+  REQUIRE(c->comm, OF_EINVAL, "of_rccl_init first");
+  REQUIRE(nslots >= 1 && nslots <= (int)c->slots.size(), OF_EINVAL, "bad slot count");
+  const int H = c->slots[0].H, W = c->slots[0].W;
+  for (int s = 0; s < nslots; ++s)
+    REQUIRE(c->slots[s].uv && c->slots[s].H == H && c->slots[s].W == W, OF_EINVAL, "slots must share one size");
+  const size_t per = 2 * (size_t)H * W;
+  float *recv = nullptr;
+  if (c->rank == 0) recv = (float *)c->arena.alloc(sizeof(float) * per * nslots * c->nranks);
+  ncclResult_t r = ncclGroupStart();
+  for (int s = 0; s < nslots && r == ncclSuccess; ++s) {
+    if (c->rank == 0) {
+      HIPCHK(hipMemcpyAsync(recv + per * s, c->slots[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
+      for (int src = 1; src < c->nranks && r == ncclSuccess; ++src)
+        r = ncclRecv(recv + per * ((size_t)src * nslots + s), per, ncclFloat, src, c->comm, c->stream);
+    } else {
+      r = ncclSend(c->slots[s].uv, per, ncclFloat, 0, c->comm, c->stream);
+    }
+  }
+  ncclResult_t r2 = ncclGroupEnd();
+  REQUIRE(r == ncclSuccess && r2 == ncclSuccess, OF_ERCCL,
+          std::string("rccl gather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  if (c->rank == 0 && out_uv_rank0)
+    HIPCHK(hipMemcpyAsync(out_uv_rank0, recv, sizeof(float) * per * nslots * c->nranks, hipMemcpyDeviceToHost,
+                          c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_rccl_finalize(of_ctx *c) {
+  if (!c) return OF_EINVAL;
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  return OF_OK;
+}
+
+// ---- stage entries ----
+int of_preprocess(of_ctx *c, const float *rgb1, const float *rgb2, int H, int W, float *gray_pair, float *lab) {
+  API_BEGIN(c)
+  REQUIRE(rgb1 && rgb2 && gray_pair, OF_EINVAL, "bad arguments");
+  const size_t n = (size_t)H * W * 3;
+  float *d1 = (float *)c->arena.alloc(sizeof(float) * n), *d2 = (float *)c->arena.alloc(sizeof(float) * n);
+  HIPCHK(hipMemcpyAsync(d1, rgb1, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d2, rgb2, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  Img gray = new_img(c, H, W, 2), g3 = new_img(c, H, W, 3);
+  uint32_t *mm = c->d_mm + 2 * 8;
+  launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
+  launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0,
+         (const float *)d1, (long)n, mm);
+  Grid2 g = grid2(H, W);
+  launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, (const float *)d1, (const float *)d2, H, W, 3, gray.p, gray.P,
+         gray.ps(), g3.p, (const uint32_t *)mm);
+  for (int ch = 0; ch < 3; ++ch) scale_img(c, view(g3, ch, 1), 0.0f, 255.0f, 9 + ch);
+  download_img(c, gray, gray_pair);
+  if (lab) download_img(c, g3, lab);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_rof_texture(of_ctx *c, const float *im, int H, int W, int C, double theta, int iters, double alp, float *out) {
+  API_BEGIN(c)
+  REQUIRE(im && out && C >= 1, OF_EINVAL, "bad arguments");
+  Img m = new_img(c, H, W, C);
+  upload_img(c, m, im);
+  Img t = rof_texture(c, m, theta, iters, alp);
+  download_img(c, t, out);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_pyramid_level(of_ctx *c, const float *im, int H, int W, int C, const double *kern, int ksize, double ratio,
+                     float *out, int *outH, int *outW) {
+  API_BEGIN(c)
+  REQUIRE(im && out && kern && ksize >= 1 && ksize <= 5 && (ksize & 1), OF_EINVAL, "bad arguments");
+  Img m = new_img(c, H, W, C);
+  upload_img(c, m, im);
+  Img o = pyramid_step(c, m, make_taps(kern, ksize, ksize), ratio);
+  download_img(c, o, out);
+  if (outH) *outH = o.H;
+  if (outW) *outW = o.W;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_resample_flow(of_ctx *c, const float *uv, int H, int W, int nH, int nW, float *out) {
+  API_BEGIN(c)
+  REQUIRE(uv && out, OF_EINVAL, "bad arguments");
+  F2 a = upload_f2(c, uv, H, W);
+  if (H == nH && W == nW) {
+    download_f2(c, a, out);
+  } else {
+    F2 b = new_f2(c, nH, nW);
+    resample_f2(c, a, b);
+    download_f2(c, b, out);
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_partial_deriv(of_ctx *c, const float *images, int H, int W, int nc, const float *uv, int interp,
+                     const double *filt, double blend, float *It, float *Ix, float *Iy) {
+  API_BEGIN(c)
+  REQUIRE(images && uv && filt && It && Ix && Iy && nc >= 1 && nc <= OF_MAX_NC, OF_EINVAL, "bad arguments");
+  REQUIRE(interp >= 0 && interp <= 2, OF_EINVAL, "Unknown interpolation method");
+  Img im = new_img(c, H, W, 2 * nc);
+  upload_img(c, im, images);
+  F2 f = upload_f2(c, uv, H, W);
+  LevelDeriv D = level_deriv(c, im, nc, interp, filt, blend);
+  Img a = new_img(c, H, W, nc), b = new_img(c, H, W, nc), d = new_img(c, H, W, nc);
+  partial_deriv(c, D, interp, f, a, b, d);
+  download_img(c, a, It);
+  download_img(c, b, Ix);
+  download_img(c, d, Iy);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_flow_operator(of_ctx *c, const of_params *P, double alpha, const float *uv, const float *duv, const float *It,
+                     const float *Ix, const float *Iy, int H, int W, int nc, float *coef, float *rhs) {
+  API_BEGIN(c)
+  REQUIRE(P && uv && It && Ix && Iy && coef && rhs && nc >= 1, OF_EINVAL, "bad arguments");
+  F2 f = upload_f2(c, uv, H, W);
+  F2 df;
+  if (duv) df = upload_f2(c, duv, H, W);
+  Img a = new_img(c, H, W, nc), b = new_img(c, H, W, nc), d = new_img(c, H, W, nc);
+  upload_img(c, a, It);
+  upload_img(c, b, Ix);
+  upload_img(c, d, Iy);
+  Img cf = new_img(c, H, W, 7);
+  F2 r = new_f2(c, H, W);
+  flow_operator(c, op_args(P, alpha, 0.0), f, duv ? &df : nullptr, a, b, d, nullptr, cf, r);
+  download_img(c, cf, coef);
+  download_f2(c, r, rhs);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_solve(of_ctx *c, const of_params *P, const float *coef, const float *rhs, int H, int W, float *x, int *iters,
+             double *rel_residual) {
+  API_BEGIN(c)
+  REQUIRE(P && coef && rhs && x, OF_EINVAL, "bad arguments");
+  check_params(P);
+  Img cf = new_img(c, H, W, 7);
+  upload_img(c, cf, coef);
+  F2 b = upload_f2(c, rhs, H, W), xx = new_f2(c, H, W);
+  SolveResult r = solve(c, P, cf, b, xx);
+  download_f2(c, xx, x);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (iters) *iters = r.iters;
+  if (rel_residual) *rel_residual = r.rel;
+  API_END(c)
+}
+
+int of_detect_occlusion(of_ctx *c, const float *uv, const float *images, int H, int W, int nc, float *occ) {
+  API_BEGIN(c)
+  REQUIRE(uv && images && occ && nc >= 1, OF_EINVAL, "bad arguments");
+  F2 f = upload_f2(c, uv, H, W), z = new_f2(c, H, W), u1 = new_f2(c, H, W);
+  fill_f2(c, z, 0.0f);
+  Img im = new_img(c, H, W, 2 * nc);
+  upload_img(c, im, images);
+  Img o = new_img(c, H, W, 1);
+  Grid2 g = grid2(H, W);
+  launch(c, "update_occ", k_update_occ, g.grid, g.block, 0, (const float2 *)f.p, (const float2 *)z.p, 0, u1.p,
+         (const float *)im.p, (const float *)im.plane(nc), nc, o.p, H, W, f.P, im.ps());
+  download_img(c, o, occ);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_weighted_median(of_ctx *c, const float *uv, const float *guide, int gc, const float *occ, int H, int W,
+                       int area_hsz, double sigma_i, float *out) {
+  API_BEGIN(c)
+  REQUIRE(uv && guide && occ && out && gc >= 1, OF_EINVAL, "bad arguments");
+  F2 f = upload_f2(c, uv, H, W), o = new_f2(c, H, W);
+  Img g = new_img(c, H, W, gc), oc = new_img(c, H, W, 1);
+  upload_img(c, g, guide);
+  upload_img(c, oc, occ);
+  wmf(c, f, g, oc.p, o, area_hsz, sigma_i);
+  download_f2(c, o, out);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+int of_median_filter(of_ctx *c, const float *in, int H, int W, int planes, int size, float *out) {
+  API_BEGIN(c)
+  REQUIRE(in && out && planes >= 1, OF_EINVAL, "bad arguments");
+  REQUIRE(size == 3 || size == 5 || size == 7, OF_ENOTSUP, "median size must be 3, 5 or 7");
+  Img a = new_img(c, H, W, planes), b = new_img(c, H, W, planes);
+  upload_img(c, a, in);
+  Grid2 g = grid2(H, W);
+  if (size == 3)
+    launch(c, "median1", k_median1<3>, gz(g, planes), g.block, 0, (const float *)a.p, b.p, H, W, a.P, a.ps());
+  else if (size == 5)
+    launch(c, "median1", k_median1<5>, gz(g, planes), g.block, 0, (const float *)a.p, b.p, H, W, a.P, a.ps());
+  else
+    launch(c, "median1", k_median1<7>, gz(g, planes), g.block, 0, (const float *)a.p, b.p, H, W, a.P, a.ps());
+  download_img(c, b, out);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+}  // extern "C"

@@ -1,0 +1,484 @@
+// kernels_flow.hip — the per-warping-iteration kernels of the IRLS loop:
+// warp + derivatives, matrix-free flow-operator assembly, update/clip +
+// occlusion, 5x5 median and the occlusion-weighted colour-guided weighted
+// median.  See DESIGN.md for the roofline of each.
+#include "kernels.h"
+
+// ---------------------------------------------------------------------------
+// cubic Hermite basis (tensor-product form of derivatives.py:7-24's
+// 16x16 bicubic coefficient matrix)
+__device__ __forceinline__ void hermite(float t, float h[4], float dh[4]) {
+  float t2 = t * t, t3 = t2 * t;
+  h[0] = 2.0f * t3 - 3.0f * t2 + 1.0f;
+  h[1] = -2.0f * t3 + 3.0f * t2;
+  h[2] = t3 - 2.0f * t2 + t;
+  h[3] = t3 - t2;
+  dh[0] = 6.0f * t2 - 6.0f * t;
+  dh[1] = -6.0f * t2 + 6.0f * t;
+  dh[2] = 3.0f * t2 - 4.0f * t + 1.0f;
+  dh[3] = 3.0f * t2 - 2.0f * t;
+}
+
+__device__ __forceinline__ float bspline3(float t) {
+  t = fabsf(t);
+  if (t < 1.0f) return 2.0f / 3.0f - t * t + 0.5f * t * t * t;
+  if (t < 2.0f) {
+    float s = 2.0f - t;
+    return s * s * s * (1.0f / 6.0f);
+  }
+  return 0.0f;
+}
+
+// partial_deriv (derivatives.py:148-296) for one pixel and all channels.
+// (x2, y2) are the 1-based warped coordinates.
+template <int INTERP>
+__device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int P, size_t ps, int i, int j, float x2,
+                                           float y2, float *it, float *ix, float *iy) {
+  const size_t k = (size_t)i * P + j;
+  if (INTERP == OF_INTERP_BICUBIC) {
+    float fx = floorf(x2), fy = floorf(y2);
+    bool oob = (fx < 1.0f) || (fx + 1.0f > (float)W) || (fy < 1.0f) || (fy + 1.0f > (float)H) || !(x2 == x2) ||
+               !(y2 == y2);
+    int fx0 = (int)fminf(fmaxf(fx, 1.0f), (float)W) - 1, cx0 = (int)fminf(fmaxf(fx + 1.0f, 1.0f), (float)W) - 1;
+    int fy0 = (int)fminf(fmaxf(fy, 1.0f), (float)H) - 1, cy0 = (int)fminf(fmaxf(fy + 1.0f, 1.0f), (float)H) - 1;
+    float ax = oob ? 0.0f : x2 - fx, ay = oob ? 0.0f : y2 - fy;
+    float hx[4], dhx[4], hy[4], dhy[4];
+    hermite(ax, hx, dhx);
+    hermite(ay, hy, dhy);
+    const size_t cs[4] = {(size_t)fy0 * P + fx0, (size_t)fy0 * P + cx0, (size_t)cy0 * P + fx0, (size_t)cy0 * P + cx0};
+    for (int c = 0; c < d.nc; ++c) {
+      const size_t o = c * ps;
+      float v = 0.0f, vx = 0.0f, vy = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int xi = q & 1, yi = q >> 1;
+        const float z = d.I2[o + cs[q]], dx = d.A[o + cs[q]], dy = d.B[o + cs[q]], dxy = d.Cc[o + cs[q]];
+        const float gx = hx[xi], gy = hy[yi], sx = hx[2 + xi], sy = hy[2 + yi];
+        v += gx * gy * z + sx * gy * dx + gx * sy * dy + sx * sy * dxy;
+        vx += dhx[xi] * gy * z + dhx[2 + xi] * gy * dx + dhx[xi] * sy * dy + dhx[2 + xi] * sy * dxy;
+        vy += gx * dhy[yi] * z + sx * dhy[yi] * dx + gx * dhy[2 + yi] * dy + sx * dhy[2 + yi] * dxy;
+      }
+      if (oob) {
+        it[c] = ix[c] = iy[c] = 0.0f;
+      } else {
+        it[c] = v - d.I1[o + k];
+        ix[c] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
+        iy[c] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
+      }
+    }
+  } else {
+    const bool out = (x2 > (float)W) || (x2 < 1.0f) || (y2 > (float)H) || (y2 < 1.0f) || !(x2 == x2) || !(y2 == y2);
+    if (out) {
+      for (int c = 0; c < d.nc; ++c) it[c] = ix[c] = iy[c] = 0.0f;
+      return;
+    }
+    const float r = y2 - 1.0f, q = x2 - 1.0f;
+    if (INTERP == OF_INTERP_CUBIC) {
+      const int i0 = (int)floorf(r), j0 = (int)floorf(q);
+      float wr[4], wc[4];
+      int rr[4], cc[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        wr[a] = bspline3(r - (float)(i0 + a - 1));
+        wc[a] = bspline3(q - (float)(j0 + a - 1));
+        rr[a] = ext_mirror(i0 + a - 1, H);
+        cc[a] = ext_mirror(j0 + a - 1, W);
+      }
+      for (int c = 0; c < d.nc; ++c) {
+        const size_t o = c * ps;
+        float v = 0.0f, vx = 0.0f, vy = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          float tv = 0.0f, tx = 0.0f, ty = 0.0f;
+          const size_t rb = o + (size_t)rr[a] * P;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            tv += wc[b] * d.Cc[rb + cc[b]];
+            tx += wc[b] * d.A[rb + cc[b]];
+            ty += wc[b] * d.B[rb + cc[b]];
+          }
+          v += wr[a] * tv;
+          vx += wr[a] * tx;
+          vy += wr[a] * ty;
+        }
+        it[c] = v - d.I1[o + k];
+        ix[c] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
+        iy[c] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
+      }
+    } else {  // bi-linear
+      int i0 = (int)floorf(r), j0 = (int)floorf(q);
+      float fr = r - i0, fc = q - j0;
+      int i1 = min(i0 + 1, H - 1), j1 = min(j0 + 1, W - 1);
+      for (int c = 0; c < d.nc; ++c) {
+        const size_t o = c * ps;
+        auto bil = [&](const float *p) {
+          const float *r0 = p + o + (size_t)i0 * P, *r1 = p + o + (size_t)i1 * P;
+          return (1.0f - fr) * ((1.0f - fc) * r0[j0] + fc * r0[j1]) + fr * ((1.0f - fc) * r1[j0] + fc * r1[j1]);
+        };
+        it[c] = bil(d.I2) - d.I1[o + k];
+        ix[c] = d.blend * bil(d.A) + (1.0f - d.blend) * d.I1x[o + k];
+        iy[c] = d.blend * bil(d.B) + (1.0f - d.blend) * d.I1y[o + k];
+      }
+    }
+  }
+}
+
+#define OF_MAX_NC 4
+
+template <int INTERP>
+__global__ void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H, int W, int P, size_t ps,
+                                float *__restrict__ It, float *__restrict__ Ix, float *__restrict__ Iy) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    float2 f = uv[k];
+    float it[OF_MAX_NC], ix[OF_MAX_NC], iy[OF_MAX_NC];
+    warp_pixel<INTERP>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, it, ix, iy);
+    for (int c = 0; c < d.nc; ++c) {
+      It[c * ps + k] = it[c];
+      Ix[c * ps + k] = ix[c];
+      Iy[c * ps + k] = iy[c];
+    }
+  }
+}
+template __global__ void k_partial_deriv<0>(DerivArgs, const float2 *, int, int, int, size_t, float *, float *, float *);
+template __global__ void k_partial_deriv<1>(DerivArgs, const float2 *, int, int, int, size_t, float *, float *, float *);
+template __global__ void k_partial_deriv<2>(DerivArgs, const float2 *, int, int, int, size_t, float *, float *, float *);
+
+// ---------------------------------------------------------------------------
+// matrix-free flow operator
+__device__ __forceinline__ float2 edge_w(const OpArgs &o, int axis, float du, float dv) {
+  float wu = 0.0f, wv = 0.0f;
+  if (o.use_q) { wu += o.aq_s * pen_w(o.qsu[axis], du); wv += o.aq_s * pen_w(o.qsv[axis], dv); }
+  if (o.use_r) { wu += o.ar_s * pen_w(o.rsu[axis], du); wv += o.ar_s * pen_w(o.rsv[axis], dv); }
+  return make_float2(wu, wv);
+}
+
+__device__ __forceinline__ float2 ld_uvd(const float2 *uv, const float2 *duv, size_t k) {
+  float2 a = uv[k];
+  if (duv) { float2 b = duv[k]; a.x += b.x; a.y += b.y; }
+  return a;
+}
+
+// coef planes: 0 wx_u, 1 wy_u, 2 wx_v, 3 wy_v, 4 a_uu, 5 a_uv, 6 a_vv; rhs float2
+__global__ void k_flow_operator(OpArgs o, const float2 *__restrict__ uv, const float2 *__restrict__ duv,
+                                const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
+                                int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
+                                float *__restrict__ coef, float2 *__restrict__ rhs) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const float2 c = ld_uvd(uv, duv, k);
+    float2 eR = make_float2(0.f, 0.f), eD = eR, eL = eR, eU = eR;
+    if (j < W - 1) { float2 n = ld_uvd(uv, duv, k + 1); eR = edge_w(o, 0, n.x - c.x, n.y - c.y); }
+    if (i < H - 1) { float2 n = ld_uvd(uv, duv, k + P); eD = edge_w(o, 1, n.x - c.x, n.y - c.y); }
+    if (j > 0) { float2 n = ld_uvd(uv, duv, k - 1); eL = edge_w(o, 0, c.x - n.x, c.y - n.y); }
+    if (i > 0) { float2 n = ld_uvd(uv, duv, k - P); eU = edge_w(o, 1, c.x - n.x, c.y - n.y); }
+    // data term, channel-averaged (classic_nl.py:330-343)
+    float du = 0.f, dv = 0.f;
+    if (duv) { du = duv[k].x; dv = duv[k].y; }
+    float psq = 0.f, psr = 0.f, ix2 = 0.f, iy2 = 0.f, ixy = 0.f, itx = 0.f, ity = 0.f;
+    for (int ch = 0; ch < nc; ++ch) {
+      const size_t kc = ch * ps + k;
+      const float gx = Ix[kc], gy = Iy[kc], itl = It[kc] + gx * du + gy * dv;
+      if (o.use_q) psq += pen_w(o.qd, itl);
+      if (o.use_r) psr += pen_w(o.rd, itl);
+      ix2 += gx * gx; iy2 += gy * gy; ixy += gx * gy;
+      itx += itl * gx; ity += itl * gy;
+    }
+    const float inv = 1.0f / (float)nc;
+    const float psi = ((o.use_q ? o.aq_d * psq : 0.f) + (o.use_r ? o.ar_d * psr : 0.f)) * inv;
+    ix2 *= inv; iy2 *= inv; ixy *= inv; itx *= inv; ity *= inv;
+    // b uses uv (not uv + duv): classic_nl.py:362-367
+    const float2 u0 = uv[k];
+    float lu = 0.f, lv = 0.f;
+    if (j < W - 1) { float2 n = uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
+    if (i < H - 1) { float2 n = uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
+    if (j > 0) { float2 n = uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
+    if (i > 0) { float2 n = uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
+    float auu = psi * ix2 + (eL.x + eR.x + eU.x + eD.x);
+    float avv = psi * iy2 + (eL.y + eR.y + eU.y + eD.y);
+    float bu = -lu - psi * itx, bv = -lv - psi * ity;
+    if (uvhat) {  // AltBA coupling (alt_ba.py:236-242)
+      const float2 h = uvhat[k];
+      const float tu = pen_w(o.rc, u0.x - h.x), tv = pen_w(o.rc, u0.y - h.y);
+      auu += o.lambda2 * tu;
+      avv += o.lambda2 * tv;
+      bu += o.lambda2 * tu * (h.x - u0.x);
+      bv += o.lambda2 * tv * (h.y - u0.y);
+    }
+    coef[k] = eR.x;
+    coef[ps + k] = eD.x;
+    coef[2 * ps + k] = eR.y;
+    coef[3 * ps + k] = eD.y;
+    coef[4 * ps + k] = auu;
+    coef[5 * ps + k] = psi * ixy;
+    coef[6 * ps + k] = avv;
+    rhs[k] = make_float2(bu, bv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// IRLS update: uv1 = uv + clip(x) (classic_nl.py:250-262); with occ != nullptr
+// also detect_occlusion(uv1, images) (occlusion.py:6-56), where uv1 at the
+// left / upper neighbour is recomputed in-register.
+__device__ __forceinline__ float2 upd(const float2 *uv, const float2 *x, size_t k, int clip) {
+  float2 a = uv[k], b = x[k];
+  if (clip) { b.x = fminf(fmaxf(b.x, -1.0f), 1.0f); b.y = fminf(fmaxf(b.y, -1.0f), 1.0f); }
+  return make_float2(a.x + b.x, a.y + b.y);
+}
+
+__global__ void k_update_occ(const float2 *__restrict__ uv, const float2 *__restrict__ x, int clip,
+                             float2 *__restrict__ uv1, const float *__restrict__ I1, const float *__restrict__ I2,
+                             int nc, float *__restrict__ occ, int H, int W, int P, size_t ps) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const float2 c = upd(uv, x, k, clip);
+    uv1[k] = c;
+    if (!occ) continue;
+    float dudx = j > 0 ? c.x - upd(uv, x, k - 1, clip).x : 0.0f;
+    float dvdy = i > 0 ? c.y - upd(uv, x, k - P, clip).y : 0.0f;
+    float div = dudx + dvdy;
+    float odiv = expf(-div * div * (1.0f / (2.0f * 0.3f * 0.3f)));
+    // bilinear warp of frame 2, 0-based, coordinates clamped ('nearest')
+    float r = fminf(fmaxf((float)i + c.y, 0.0f), (float)(H - 1));
+    float q = fminf(fmaxf((float)j + c.x, 0.0f), (float)(W - 1));
+    int i0 = (int)floorf(r), j0 = (int)floorf(q);
+    float fr = r - i0, fc = q - j0;
+    int i1 = min(i0 + 1, H - 1), j1 = min(j0 + 1, W - 1);
+    float it = 0.0f;
+    for (int ch = 0; ch < nc; ++ch) {
+      const float *b = I2 + ch * ps;
+      const float *r0 = b + (size_t)i0 * P, *r1 = b + (size_t)i1 * P;
+      float w = (1.0f - fr) * ((1.0f - fc) * r0[j0] + fc * r0[j1]) + fr * ((1.0f - fc) * r1[j0] + fc * r1[j1]);
+      it += fabsf(w - I1[ch * ps + k]);
+    }
+    if (nc > 1) it /= (float)nc;
+    occ[k] = odiv * expf(-it * it * (1.0f / (2.0f * 20.0f * 20.0f)));
+  }
+}
+
+// in-place uv += x (HS, hs.py:130-134), optional clip
+__global__ void k_add_update(float2 *__restrict__ uv, const float2 *__restrict__ x, int clip, int H, int W, int P) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    uv[k] = upd(uv, x, k, clip);
+  }
+}
+
+// uv = uv + (b - a): the duv bookkeeping of classic_nl.py:271-275 / ba.py:404-407
+__global__ void k_axpy_diff(float2 *__restrict__ uv, const float2 *__restrict__ a, const float2 *__restrict__ b, int H,
+                            int W, int P) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    float2 u = uv[k], x = a[k], y = b[k];
+    uv[k] = make_float2(u.x + (y.x - x.x), u.y + (y.y - x.y));
+  }
+}
+
+// out = b - a
+__global__ void k_sub2(const float2 *__restrict__ a, const float2 *__restrict__ b, float2 *__restrict__ out, int H,
+                       int W, int P) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    float2 x = a[k], y = b[k];
+    out[k] = make_float2(y.x - x.x, y.y - x.y);
+  }
+}
+
+// sum of squares of a float2 field (HS early exit ||x||_2 < 1e-3, hs.py:127)
+__global__ void k_norm2(const float2 *__restrict__ x, int H, int W, int P, double *partials, unsigned *counter,
+                        double *result) {
+  __shared__ double lds[16];
+  double v[1] = {0.0};
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    float2 a = x[(size_t)i * P + j];
+    v[0] += (double)a.x * a.x + (double)a.y * a.y;
+  }
+  block_sum<1>(v, lds);
+  const int nb = gridDim.x * gridDim.y;
+  if (arrive_last<1>(v, partials, counter, nb, blockIdx.x + blockIdx.y * gridDim.x)) {
+    double s[1];
+    final_sum<1>(s, partials, nb, lds);
+    if (threadIdx.x == 0 && threadIdx.y == 0) {
+      *result = s[0];
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scipy.ndimage.median_filter(size=S, mode='reflect'): rank selection with
+// index tie-break (the element of rank S*S/2), branch-free.
+template <int S>
+__device__ __forceinline__ float median_window(const float *a) {
+  constexpr int N = S * S;
+  float m = a[0];
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < N; ++u) cnt += (a[u] < a[t]) || (a[u] == a[t] && u < t);
+    m = cnt == N / 2 ? a[t] : m;
+  }
+  return m;
+}
+
+template <int S>
+__global__ void k_median2(const float2 *__restrict__ in, float2 *__restrict__ out, int H, int W, int P) {
+  constexpr int h = S / 2;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    float au[S * S], av[S * S];
+    int t = 0;
+#pragma unroll
+    for (int a = -h; a <= h; ++a) {
+      const float2 *row = in + (size_t)ext_reflect(i + a, H) * P;
+#pragma unroll
+      for (int b = -h; b <= h; ++b, ++t) {
+        float2 v = row[ext_reflect(j + b, W)];
+        au[t] = v.x;
+        av[t] = v.y;
+      }
+    }
+    out[(size_t)i * P + j] = make_float2(median_window<S>(au), median_window<S>(av));
+  }
+}
+
+template <int S>
+__global__ void k_median1(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps) {
+  constexpr int h = S / 2;
+  in += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    float a[S * S];
+    int t = 0;
+#pragma unroll
+    for (int y = -h; y <= h; ++y) {
+      const float *row = in + (size_t)ext_reflect(i + y, H) * P;
+#pragma unroll
+      for (int x = -h; x <= h; ++x, ++t) a[t] = row[ext_reflect(j + x, W)];
+    }
+    out[(size_t)i * P + j] = median_window<S>(a);
+  }
+}
+template __global__ void k_median2<3>(const float2 *, float2 *, int, int, int);
+template __global__ void k_median2<5>(const float2 *, float2 *, int, int, int);
+template __global__ void k_median2<7>(const float2 *, float2 *, int, int, int);
+template __global__ void k_median1<3>(const float *, float *, int, int, int, size_t);
+template __global__ void k_median1<5>(const float *, float *, int, int, int, size_t);
+template __global__ void k_median1<7>(const float *, float *, int, int, int, size_t);
+
+// uv_tilde = u + lam * (un - u) (denoise_LO, denoising.py:28-29)
+__global__ void k_lo_blend(const float2 *__restrict__ u, const float2 *__restrict__ un, float lam,
+                           float2 *__restrict__ out, int H, int W, int P) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    float2 a = u[k], b = un[k];
+    out[k] = make_float2(a.x + lam * (b.x - a.x), a.y + lam * (b.y - a.y));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Occlusion-weighted, colour-guided weighted median
+// (weighted_median.py:24-112).  One wave per 8x8 output tile:
+//  1. stage the (8+2h)^2 region (whole-sample mirror padding = np.pad
+//     'reflect') in LDS: u, v sort keys, guide channels, occlusion;
+//  2. bitonic-sort the u keys and the v keys once per tile;
+//  3. every lane (output pixel) sums its window weights, then walks the
+//     sorted region list in lockstep with the other lanes (broadcast LDS
+//     reads), accumulating only samples inside its own window, and stops at
+//     the first sample whose cumulative weight reaches half the total:
+//     exactly np.searchsorted(cumsum(w_sorted), total / 2).
+#define WMF_T 8
+template <int GC>
+__global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
+                                            const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
+                                            int P, size_t ps, int hsz, float inv2s2, int RW, int nreg, int npow2) {
+  extern __shared__ uint64_t lds_u64[];
+  uint64_t *ku = lds_u64, *kv = lds_u64 + npow2;
+  float *smp = reinterpret_cast<float *>(lds_u64 + 2 * npow2);  // [GC+1][nreg]
+  const int ty0 = blockIdx.y * WMF_T, tx0 = blockIdx.x * WMF_T;
+  const int t = threadIdx.x;
+  for (int s = t; s < npow2; s += 64) {
+    if (s < nreg) {
+      const int ry = s / RW, rx = s - ry * RW;
+      const size_t g = (size_t)ext_mirror(ty0 - hsz + ry, H) * P + ext_mirror(tx0 - hsz + rx, W);
+      const float2 v = uv[g];
+      const uint64_t lo = ((uint64_t)ry << 16) | (uint64_t)rx;
+      ku[s] = ((uint64_t)f2ord(v.x) << 32) | lo;
+      kv[s] = ((uint64_t)f2ord(v.y) << 32) | lo;
+#pragma unroll
+      for (int c = 0; c < GC; ++c) smp[c * nreg + s] = guide[c * ps + g];
+      smp[GC * nreg + s] = occ[g];
+    } else {
+      ku[s] = ~0ull;
+      kv[s] = ~0ull;
+    }
+  }
+  __syncthreads();
+  for (int kk = 2; kk <= npow2; kk <<= 1)
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (int idx = t; idx < npow2; idx += 64) {
+        const int ixj = idx ^ jj;
+        if (ixj > idx) {
+          const bool up = (idx & kk) == 0;
+          uint64_t a = ku[idx], b = ku[ixj];
+          if ((a > b) == up) { ku[idx] = b; ku[ixj] = a; }
+          a = kv[idx];
+          b = kv[ixj];
+          if ((a > b) == up) { kv[idx] = b; kv[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  const int py = t >> 3, px = t & 7;
+  const int gi = ty0 + py, gj = tx0 + px;
+  if (gi >= H || gj >= W) return;
+  const int cy = py + hsz, cx = px + hsz;
+  float cg[GC];
+#pragma unroll
+  for (int c = 0; c < GC; ++c) cg[c] = smp[c * nreg + cy * RW + cx];
+  auto weight = [&](int s) {
+    float d2 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < GC; ++c) {
+      const float e = smp[c * nreg + s] - cg[c];
+      d2 += e * e;
+    }
+    return fmaxf(expf(-d2 * inv2s2) * smp[GC * nreg + s], 1e-10f);
+  };
+  double tot = 0.0;
+  for (int dy = -hsz; dy <= hsz; ++dy)
+    for (int dx = -hsz; dx <= hsz; ++dx) tot += (double)weight((cy + dy) * RW + cx + dx);
+  const double half = 0.5 * tot;
+  float res[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int comp = 0; comp < 2; ++comp) {
+    const uint64_t *keys = comp ? kv : ku;
+    double cum = 0.0;
+    float last = 0.0f;
+    for (int k = 0; k < nreg; ++k) {
+      const uint64_t key = keys[k];
+      const int ry = (int)((key >> 16) & 0xffff), rx = (int)(key & 0xffff);
+      if (abs(ry - cy) <= hsz && abs(rx - cx) <= hsz) {
+        last = ord2f((uint32_t)(key >> 32));
+        cum += (double)weight(ry * RW + rx);
+        if (cum >= half) break;
+      }
+    }
+    res[comp] = last;
+  }
+  out[(size_t)gi * P + gj] = make_float2(res[0], res[1]);
+}
+template __global__ void k_wmf<1>(const float2 *, const float *, const float *, float2 *, int, int, int, size_t, int,
+                                  float, int, int, int);
+template __global__ void k_wmf<3>(const float2 *, const float *, const float *, float2 *, int, int, int, size_t, int,
+                                  float, int, int, int);

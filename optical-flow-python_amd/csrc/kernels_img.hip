@@ -1,0 +1,253 @@
+// kernels_img.hip — image-side kernels: colour conversion, global min/max,
+// scaling, ROF structure-texture split, correlation, bilinear resize and the
+// cubic B-spline prefilter.  All are HBM-streaming stencils (no MFMA).
+#include "kernels.h"
+
+// ---------------------------------------------------------------------------
+// global min / max (scale_image, image_processing.py:6-26)
+// mm[0] = ordered-uint min, mm[1] = ordered-uint max (init by k_mm_init)
+__global__ void k_mm_init(uint32_t *mm, int n) {
+  int t = threadIdx.x;
+  if (t < n) { mm[2 * t] = 0xffffffffu; mm[2 * t + 1] = 0u; }
+}
+
+// min/max over `planes` pitched planes; one result pair per launch (slot)
+__global__ void k_minmax(const float *__restrict__ a, int H, int W, int P, int planes, size_t plane_stride,
+                         uint32_t *mm) {
+  uint32_t lo = 0xffffffffu, hi = 0u;
+  OF_FOR_PIXELS(H, W) {
+    if (j < W)
+      for (int c = 0; c < planes; ++c) {
+        uint32_t o = f2ord(a[c * plane_stride + (size_t)i * P + j]);
+        lo = min(lo, o);
+        hi = max(hi, o);
+      }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_down((int)lo, off, 64));
+    hi = max(hi, (uint32_t)__shfl_down((int)hi, off, 64));
+  }
+  if (((threadIdx.x + threadIdx.y * blockDim.x) & 63) == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+// x -> (x - lo) / (hi - lo) * (vhigh - vlow) + vlow, or the midpoint when hi == lo
+__global__ void k_scale(float *__restrict__ a, int H, int W, int P, int planes, size_t plane_stride,
+                        const uint32_t *mm, float vlow, float vhigh) {
+  const float lo = ord2f(mm[0]), hi = ord2f(mm[1]);
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    for (int c = 0; c < planes; ++c) {
+      float &x = a[c * plane_stride + (size_t)i * P + j];
+      x = hi == lo ? (vlow + vhigh) * 0.5f : (x - lo) / (hi - lo) * (vhigh - vlow) + vlow;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// colour conversion (interface.py:74-141).  rgb: interleaved H x W x C dense.
+__global__ void k_rgb_max(const float *__restrict__ rgb, long n, uint32_t *mm) {
+  uint32_t hi = 0u;
+  for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x)
+    hi = max(hi, f2ord(rgb[k]));
+  for (int off = 32; off > 0; off >>= 1) hi = max(hi, (uint32_t)__shfl_down((int)hi, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(&mm[1], hi);
+}
+
+__device__ __forceinline__ float q_u8(float x) {
+  float q = floorf(x + 0.5f);
+  return fminf(fmaxf(q, 0.0f), 255.0f);
+}
+
+// gray (uint8 round trip) of both frames; Lab of frame 1 when lab != nullptr
+__global__ void k_rgb_prep(const float *__restrict__ rgb1, const float *__restrict__ rgb2, int H, int W, int C,
+                           float *gray, int P, size_t ps, float *lab, const uint32_t *mm_rgbmax) {
+  const bool norm = ord2f(mm_rgbmax[1]) > 1.0f;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    size_t k = (size_t)i * W + j, o = (size_t)i * P + j;
+    if (C == 1) {
+      gray[o] = rgb1[k];
+      gray[ps + o] = rgb2[k];
+      if (lab) lab[o] = rgb1[k];
+      continue;
+    }
+    const float *a = rgb1 + 3 * k, *b = rgb2 + 3 * k;
+    gray[o] = floorf(0.2989f * q_u8(a[0]) + 0.5870f * q_u8(a[1]) + 0.1140f * q_u8(a[2]) + 0.5f);
+    gray[ps + o] = floorf(0.2989f * q_u8(b[0]) + 0.5870f * q_u8(b[1]) + 0.1140f * q_u8(b[2]) + 0.5f);
+    if (!lab) continue;
+    float R = a[0], G = a[1], B = a[2];
+    if (norm) { R /= 255.0f; G /= 255.0f; B /= 255.0f; }
+    const float T = 0.008856f;
+    float X = (0.412453f * R + 0.357580f * G + 0.180423f * B) / 0.950456f;
+    float Y = 0.212671f * R + 0.715160f * G + 0.072169f * B;
+    float Z = (0.019334f * R + 0.119193f * G + 0.950227f * B) / 1.088754f;
+    float Y3 = cbrtf(Y);
+    float fX = X > T ? cbrtf(X) : 7.787f * X + 16.0f / 116.0f;
+    float fY = Y > T ? Y3 : 7.787f * Y + 16.0f / 116.0f;
+    float fZ = Z > T ? cbrtf(Z) : 7.787f * Z + 16.0f / 116.0f;
+    lab[o] = Y > T ? 116.0f * Y3 - 16.0f : 903.3f * Y;
+    lab[ps + o] = 500.0f * (fX - fY);
+    lab[2 * ps + o] = 200.0f * (fY - fZ);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ROF primal-dual iteration (image_processing.py:86-136), one channel per
+// blockIdx.z.  p: float2 {p_x, p_y} per pixel; ping-pong pin -> pout.
+__device__ __forceinline__ float rof_div(const float2 *__restrict__ p, int i, int j, int P) {
+  const float2 c = p[(size_t)i * P + j];
+  float d = j > 0 ? c.x - p[(size_t)i * P + j - 1].x : c.x;
+  d += i > 0 ? c.y - p[(size_t)(i - 1) * P + j].y : c.y;
+  return d;
+}
+
+__global__ void k_rof_iter(const float *__restrict__ im, const float2 *__restrict__ pin, float2 *__restrict__ pout,
+                           int H, int W, int P, size_t ps, float theta, float delta) {
+  im += blockIdx.z * ps;
+  pin += blockIdx.z * ps;
+  pout += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    size_t k = (size_t)i * P + j;
+    float u = im[k] + theta * rof_div(pin, i, j, P);
+    float gx = j < W - 1 ? im[k + 1] + theta * rof_div(pin, i, j + 1, P) - u : 0.0f;
+    float gy = i < H - 1 ? im[k + P] + theta * rof_div(pin, i + 1, j, P) - u : 0.0f;
+    float2 q = pin[k];
+    float a = q.x + delta * gx, b = q.y + delta * gy;
+    float nrm = fmaxf(sqrtf(a * a + b * b), 1.0f);
+    pout[k] = make_float2(a / nrm, b / nrm);
+  }
+}
+
+// texture = im_norm - alp * (im_norm + theta div p)
+__global__ void k_rof_final(const float *__restrict__ im, const float2 *__restrict__ p, float *__restrict__ out,
+                            int H, int W, int P, size_t ps, float theta, float alp) {
+  im += blockIdx.z * ps;
+  p += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    size_t k = (size_t)i * P + j;
+    out[k] = im[k] - alp * (im[k] + theta * rof_div(p, i, j, P));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scipy.ndimage.correlate(mode='reflect') with an odd kh x kw kernel, per plane z
+__global__ void k_correlate(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps,
+                            Taps t) {
+  in += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  const int ch = t.kh / 2, cw = t.kw / 2;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    float s = 0.0f;
+    for (int a = 0; a < t.kh; ++a) {
+      const float *row = in + (size_t)ext_reflect(i + a - ch, H) * P;
+      for (int b = 0; b < t.kw; ++b) {
+        float w = t.w[a * t.kw + b];
+        if (w != 0.0f) s += w * row[ext_reflect(j + b - cw, W)];
+      }
+    }
+    out[(size_t)i * P + j] = s;
+  }
+}
+
+// _matlab_imresize_bilinear / resample_flow: source coordinate
+// (o + 0.5) * (H / nH) - 0.5 clipped to [0, H-1], bilinear, times `mult`.
+template <typename T>
+__global__ void k_resize(const T *__restrict__ in, int H, int W, int P, size_t ps, T *__restrict__ out, int nH, int nW,
+                         int nP, size_t nps, float mult) {
+  in += blockIdx.z * ps;
+  out += blockIdx.z * nps;
+  const float sy = (float)H / (float)nH, sx = (float)W / (float)nW;
+  const int j = blockIdx.x * OF_BX + threadIdx.x;
+  if (j >= nW) return;
+  float c = fminf(fmaxf((j + 0.5f) * sx - 0.5f, 0.0f), (float)(W - 1));
+  int j0 = (int)floorf(c);
+  float fc = c - j0;
+  int j1 = min(j0 + 1, W - 1);
+  for (int o = blockIdx.y * OF_BY + threadIdx.y; o < nH; o += gridDim.y * OF_BY) {
+    float r = fminf(fmaxf((o + 0.5f) * sy - 0.5f, 0.0f), (float)(H - 1));
+    int i0 = (int)floorf(r);
+    float fr = r - i0;
+    int i1 = min(i0 + 1, H - 1);
+    const T *r0 = in + (size_t)i0 * P, *r1 = in + (size_t)i1 * P;
+    T v = (1.0f - fr) * ((1.0f - fc) * r0[j0] + fc * r0[j1]) + fr * ((1.0f - fc) * r1[j0] + fc * r1[j1]);
+    out[(size_t)o * nP + j] = mult * v;
+  }
+}
+template __global__ void k_resize<float>(const float *, int, int, int, size_t, float *, int, int, int, size_t, float);
+template __global__ void k_resize<float2>(const float2 *, int, int, int, size_t, float2 *, int, int, int, size_t,
+                                          float);
+
+// ---------------------------------------------------------------------------
+// cubic B-spline prefilter with mirror boundary = the symmetric IIR
+// 6 / (z + 4 + 1/z) realised as a truncated FIR h[k] = c0 * zp^|k|,
+// zp = sqrt(3) - 2, c0 = -6 zp / (1 - zp^2), |k| <= OF_BSPL_K (zp^16 ~ 7e-10)
+__global__ void k_bspline_rows(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps,
+                               BsplTaps t) {
+  in += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const float *row = in + (size_t)i * P;
+    float s = t.h[0] * row[j];
+    for (int k = 1; k <= OF_BSPL_K; ++k) s += t.h[k] * (row[ext_mirror(j - k, W)] + row[ext_mirror(j + k, W)]);
+    out[(size_t)i * P + j] = s;
+  }
+}
+__global__ void k_bspline_cols(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps,
+                               BsplTaps t) {
+  in += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    float s = t.h[0] * in[(size_t)i * P + j];
+    for (int k = 1; k <= OF_BSPL_K; ++k)
+      s += t.h[k] * (in[(size_t)ext_mirror(i - k, H) * P + j] + in[(size_t)ext_mirror(i + k, H) * P + j]);
+    out[(size_t)i * P + j] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// layout converters between dense planar host images and pitched device data
+__global__ void k_planar2_to_f2(const float *__restrict__ a, float2 *__restrict__ out, int H, int W, int P,
+                                size_t dense_ps) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    size_t k = (size_t)i * W + j;
+    out[(size_t)i * P + j] = make_float2(a[k], a[dense_ps + k]);
+  }
+}
+__global__ void k_f2_to_planar2(const float2 *__restrict__ in, float *__restrict__ a, int H, int W, int P,
+                                size_t dense_ps) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    size_t k = (size_t)i * W + j;
+    float2 v = in[(size_t)i * P + j];
+    a[k] = v.x;
+    a[dense_ps + k] = v.y;
+  }
+}
+__global__ void k_fill_f2(float2 *out, int H, int W, int P, float2 v) {
+  OF_FOR_PIXELS(H, W) {
+    if (j < W) out[(size_t)i * P + j] = v;
+  }
+}
+
+// out = a - alp * b per plane (fc pre-filter)
+__global__ void k_sub_scaled(const float *__restrict__ a, const float *__restrict__ b, float alp,
+                             float *__restrict__ out, int H, int W, int P, size_t ps) {
+  a += blockIdx.z * ps;
+  b += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    out[k] = a[k] - alp * b[k];
+  }
+}

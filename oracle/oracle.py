@@ -1,0 +1,265 @@
+"""TEST INFRASTRUCTURE: ctypes wrapper of the float64 CPU restatement
+(oracle/optflow_oracle.c).  Imported only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg, as the checker.  Functions take and return
+numpy arrays in the reference's (H, W, C) layout and mirror the reference's
+function signatures.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "optical-flow-python_amd"))
+from optical_flow import _abi  # noqa: E402  (struct layout only)
+
+LIB = os.path.join(HERE, "liboptflow_oracle.so")
+_lib = None
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.ofr_penalty.restype = C.c_double
+        _lib.ofr_penalty.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.c_int]
+        _lib.ofr_compute_flow.argtypes = [C.POINTER(_abi.OfParams), _dp, C.c_int, C.c_int, C.c_int, _dp, C.c_int,
+                                          _dp, _dp, C.POINTER(_abi.OfStats)]
+        _lib.ofr_estimate_flow.argtypes = [C.POINTER(_abi.OfParams), _dp, _dp, C.c_int, C.c_int, C.c_int, _dp, _dp,
+                                           C.POINTER(_abi.OfStats)]
+        _lib.ofr_flow_operator.argtypes = [C.POINTER(_abi.OfParams), C.c_double, _dp, _dp, _dp, _dp, _dp, C.c_int,
+                                           C.c_int, C.c_int, _dp, _dp]
+        _lib.ofr_solve.argtypes = [C.POINTER(_abi.OfParams), _dp, _dp, C.c_int, C.c_int, _dp, _ip, _dp]
+        _lib.ofr_num_threads.restype = C.c_int
+    return _lib
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def planar(a):
+    a = np.asarray(a, dtype=np.float64)
+    return _d(a[None] if a.ndim == 2 else np.moveaxis(a, 2, 0))
+
+
+def unplanar(a, squeeze=True):
+    if squeeze and a.shape[0] == 1:
+        return a[0]
+    return np.moveaxis(a, 0, 2).copy()
+
+
+def num_threads():
+    return lib().ofr_num_threads()
+
+
+def penalty(kind, params, x, d):
+    x = _d(np.atleast_1d(x))
+    y = np.empty_like(x)
+    p = list(np.atleast_1d(params)) + [0.0]
+    k = _abi.PENALTY[kind] if isinstance(kind, str) else kind
+    lib().ofr_penalty_array(C.c_int(k), C.c_double(p[0]), C.c_double(p[1]), C.c_int(d), _p(x), _p(y),
+                            C.c_long(x.size))
+    return y
+
+
+def rgb2gray(rgb):
+    rgb = _d(rgb)
+    H, W = rgb.shape[:2]
+    out = np.empty((H, W))
+    lib().ofr_rgb2gray(_p(rgb), H, W, _p(out))
+    return out
+
+
+def rgb2lab(rgb):
+    rgb = _d(rgb)
+    H, W = rgb.shape[:2]
+    out = np.empty((3, H, W))
+    lib().ofr_rgb2lab(_p(rgb), H, W, _p(out))
+    return unplanar(out)
+
+
+def scale_image(im, lo, hi):
+    a = _d(im).copy()
+    lib().ofr_scale_image(_p(a), C.c_long(a.size), C.c_double(lo), C.c_double(hi))
+    return a
+
+
+def rof_texture(im, theta=1.0 / 8, iters=100, alp=0.95):
+    p = planar(im)
+    out = np.empty_like(p)
+    lib().ofr_rof_texture(_p(p), p.shape[1], p.shape[2], p.shape[0], C.c_double(theta), iters, C.c_double(alp),
+                          _p(out))
+    return unplanar(out, np.asarray(im).ndim == 2)
+
+
+def gaussian(size, sigma):
+    k = np.empty((size, size))
+    lib().ofr_gaussian(size, C.c_double(sigma), _p(k))
+    return k
+
+
+def correlate(a, k):
+    a, k = _d(a), _d(k)
+    out = np.empty_like(a)
+    lib().ofr_correlate(_p(a), a.shape[0], a.shape[1], _p(k), k.shape[0], k.shape[1], _p(out))
+    return out
+
+
+def pyramid(img, f, n_levels, ratio):
+    img = np.asarray(img, dtype=np.float64)
+    f = _d(f)
+    out = [img.copy()]
+    cur = planar(img)
+    for _ in range(1, n_levels):
+        H, W = cur.shape[1:]
+        nH, nW = C.c_int(), C.c_int()
+        lib().ofr_resize_dims(H, W, C.c_double(ratio), C.byref(nH), C.byref(nW))
+        nxt = np.empty((cur.shape[0], nH.value, nW.value))
+        lib().ofr_pyramid_level(_p(cur), H, W, cur.shape[0], _p(f), f.shape[0], C.c_double(ratio), _p(nxt),
+                                C.byref(nH), C.byref(nW))
+        cur = nxt
+        out.append(unplanar(cur, img.ndim == 2))
+    return out
+
+
+def resample_flow(uv, sz):
+    p = planar(uv)
+    out = np.empty((2, sz[0], sz[1]))
+    lib().ofr_resample_flow(_p(p), p.shape[1], p.shape[2], sz[0], sz[1], _p(out))
+    return unplanar(out, False)
+
+
+def interp2_bicubic(Z, XI, YI, filt):
+    Z, XI, YI = _d(Z), _d(XI), _d(YI)
+    outs = [np.empty(XI.shape) for _ in range(3)]
+    lib().ofr_interp2_bicubic(_p(Z), Z.shape[0], Z.shape[1], _p(XI), _p(YI), C.c_long(XI.size), _p(_d(filt)),
+                              *[_p(o) for o in outs])
+    return tuple(outs)
+
+
+def bspline_prefilter(a):
+    a = _d(a)
+    out = np.empty_like(a)
+    lib().ofr_bspline_prefilter(_p(a), a.shape[0], a.shape[1], _p(out))
+    return out
+
+
+def partial_deriv(images, uv, interp='cubic', filt=None, blend=0.5):
+    if filt is None:
+        filt = np.array([1, -8, 0, 8, -1]) / 12.0
+    im = planar(images)
+    nc = im.shape[0] // 2
+    H, W = im.shape[1:]
+    outs = [np.empty((nc, H, W)) for _ in range(3)]
+    lib().ofr_partial_deriv(_p(im), H, W, nc, _p(planar(uv)), _abi.INTERP[interp], _p(_d(filt)), C.c_double(blend),
+                            *[_p(o) for o in outs])
+    return tuple(unplanar(o) for o in outs)
+
+
+def flow_operator(P, alpha, uv, duv, It, Ix, Iy):
+    """Matrix-free operator planes (7, H, W) and rhs (2, H, W)."""
+    uvp = planar(uv)
+    H, W = uvp.shape[1:]
+    itp = planar(It)
+    nc = itp.shape[0]
+    coef = np.empty((7, H, W))
+    rhs = np.empty((2, H, W))
+    lib().ofr_flow_operator(C.byref(P), C.c_double(alpha), _p(uvp), _p(None if duv is None else planar(duv)),
+                            _p(itp), _p(planar(Ix)), _p(planar(Iy)), H, W, nc, _p(coef), _p(rhs))
+    return coef, rhs
+
+
+def solve(P, coef, rhs):
+    coef, rhs = _d(coef), _d(rhs)
+    H, W = coef.shape[1:]
+    x = np.empty((2, H, W))
+    it = C.c_int()
+    rr = C.c_double()
+    lib().ofr_solve(C.byref(P), _p(coef), _p(rhs), H, W, _p(x), C.byref(it), C.byref(rr))
+    return x, it.value, rr.value
+
+
+def detect_occlusion(uv, images):
+    im = planar(images)
+    H, W = im.shape[1:]
+    out = np.empty((H, W))
+    lib().ofr_detect_occlusion(_p(planar(uv)), _p(im), H, W, im.shape[0] // 2, _p(out))
+    return out
+
+
+def weighted_median(uv, guide, occ, hsz, sigma_i, mfsz=5):
+    uvp = planar(uv)
+    H, W = uvp.shape[1:]
+    g = None if guide is None else planar(guide)
+    out = np.empty((2, H, W))
+    lib().ofr_weighted_median(_p(uvp), _p(g), 0 if g is None else g.shape[0], _p(_d(occ)), H, W, hsz,
+                              C.c_double(sigma_i), mfsz, _p(out))
+    return unplanar(out, False)
+
+
+def median_filter(a, size=5):
+    p = planar(a)
+    out = np.empty_like(p)
+    lib().ofr_median_filter(_p(p), p.shape[1], p.shape[2], p.shape[0], size, _p(out))
+    return unplanar(out, np.asarray(a).ndim == 2)
+
+
+def compute_flow(ope, init=None):
+    """compute_flow() of a method object (its attribute bag -> of_params)."""
+    P = ope.to_params()
+    im = planar(ope.images)
+    H, W = im.shape[1:]
+    g, gc = None, 0
+    if ope._METHOD == 'classic_nl' and ope.color_images is not None:
+        gg = np.asarray(ope.color_images, dtype=float)
+        if gg.shape[:2] == (H, W):
+            g = planar(gg)
+            gc = g.shape[0]
+    out = np.empty((2, H, W))
+    st = _abi.OfStats()
+    lib().ofr_compute_flow(C.byref(P), _p(im), H, W, im.shape[0] // 2, _p(g), gc,
+                           _p(None if init is None else planar(init)), _p(out), C.byref(st))
+    ope.alpha = P.alpha
+    return unplanar(out, False), st
+
+
+def estimate_flow(im1, im2, method='classic+nl-fast', params=None, solver=None):
+    """estimate_flow() through the oracle (same registry as the product)."""
+    from optical_flow.methods.config import load_of_method
+    im1 = np.asarray(im1, dtype=float)
+    im2 = np.asarray(im2, dtype=float)
+    ope = load_of_method(method)
+    if params is not None:
+        ope.parse_input_parameter(params)
+    if solver is not None:
+        ope.solver = solver
+    H, W = im1.shape[:2]
+    if im1.ndim == 3 and im1.shape[2] < 3:
+        ope.images = np.concatenate([im1, im2], axis=2)
+        if ope.color_images is not None:
+            ope.color_images = im1.copy()
+        return compute_flow(ope)[0]
+    P = ope.to_params()
+    P.guide_mode = int(ope._METHOD == 'classic_nl' and ope.color_images is not None)
+    Cc = 3 if im1.ndim == 3 else 1
+    a = _d(im1[:, :, :3] if Cc == 3 else im1)
+    b = _d(im2[:, :, :3] if Cc == 3 else im2)
+    out = np.empty((2, H, W))
+    st = _abi.OfStats()
+    lib().ofr_estimate_flow(C.byref(P), _p(a), _p(b), H, W, Cc, None, _p(out), C.byref(st))
+    return unplanar(out, False)

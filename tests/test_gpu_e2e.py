@@ -1,0 +1,96 @@
+"""GPU end-to-end parity: estimate_flow on the GPU vs the reference outputs
+(golden) and the float64 oracle.
+
+The pipeline is non-smooth (clipping + medians), so u/v parity is stated
+statistically: mean / median / p99 end-point difference to the
+reference flow, and |delta AEPE| against ground truth."""
+import numpy as np
+import pytest
+
+from conftest import epe_stats
+
+pytestmark = pytest.mark.gpu
+
+METHODS = ["classic+nl-fast", "classic+nl", "classic+nl-full", "hs-brightness", "hs", "ba-brightness", "ba",
+           "classic-l", "classic-c-a", "classic-c-brightness", "classic-c", "classic++"]
+
+
+def _aepe(uv, gt):
+    return float(np.sqrt(((uv - gt) ** 2).sum(-1)).mean())
+
+
+# Tolerances per method family, from measurement (DESIGN.md "Parity"):
+#  - stable (HS, BA-Lorentzian): float32 vs float64 only;
+#  - Classic+NL: weighted median over 225 samples (fp32 weights may pick a
+#    neighbouring order statistic);
+#  - charbonnier (classic-c*, classic++): chaotic in the reference itself -
+#    perturbing its direct solve by 1e-12 (relative) moves its own output by
+#    4.7e-3 / 5.4e-3 px mean on this crop;
+#  - classic-c-a: the reference diverges (|uv| ~ 3.6e36); so must we.
+TOL = {"stable": (1e-3, 2e-4), "nl": (1e-2, 2e-3), "chaotic": (3e-2, 2e-2)}
+FAMILY = {"classic+nl-fast": "nl", "classic+nl": "nl", "classic+nl-full": "nl", "hs-brightness": "stable",
+          "hs": "stable", "ba-brightness": "stable", "ba": "stable", "classic-l": "stable",
+          "classic-c-brightness": "chaotic", "classic-c": "chaotic", "classic++": "chaotic"}
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_e2e_small_crop(golden, method):
+    import optical_flow
+    d = golden("e2e_small.npz")
+    uv = optical_flow.estimate_flow(d["im1"], d["im2"], method)
+    if method == "classic-c-a":
+        assert np.abs(d[method]).max() > 1e20
+        assert (~np.isfinite(uv)).any() or np.abs(uv).max() > 1e20
+        return
+    s = epe_stats(uv, d[method])
+    print(method, s)
+    assert np.all(np.isfinite(uv))
+    mean_tol, med_tol = TOL[FAMILY[method]]
+    assert s["mean"] < mean_tol and s["median"] < med_tol, s
+
+
+def test_e2e_gray_and_pcg(golden):
+    import optical_flow
+    d = golden("e2e_small.npz")
+    for key, args in (("gray:classic+nl-fast", (d["gray1"], d["gray2"], "classic+nl-fast")),
+                      ("gray:hs-brightness", (d["gray1"], d["gray2"], "hs-brightness"))):
+        s = epe_stats(optical_flow.estimate_flow(*args), d[key])
+        assert s["mean"] < 2e-2, (key, s)
+    uv = optical_flow.estimate_flow(d["im1"], d["im2"], "classic+nl-fast", {"solver": "pcg"})
+    assert epe_stats(uv, d["pcg:classic+nl-fast"])["mean"] < 3e-2
+    uv = optical_flow.estimate_flow(d["im1"], d["im2"], "hs", {"solver": "pcg"})
+    assert epe_stats(uv, d["pcg:hs"])["mean"] < 3e-2
+
+
+@pytest.mark.parametrize("method", ["classic+nl-fast", "hs", "classic-c", "hs-brightness"])
+def test_e2e_synthetic(golden, method):
+    import optical_flow
+    d = golden("e2e_synth.npz")
+    uv = optical_flow.estimate_flow(d["im1"], d["im2"], method)
+    s = epe_stats(uv, d[method])
+    da = abs(_aepe(uv, d["gt"]) - _aepe(d[method], d["gt"]))
+    print(method, s, "dAEPE", da)
+    fam = {"classic+nl-fast": "nl", "hs": "stable", "hs-brightness": "stable", "classic-c": "chaotic"}[method]
+    mean_tol, med_tol = TOL[fam]
+    assert s["mean"] < mean_tol and s["median"] < med_tol, s
+    assert da < (3e-3 if fam == "chaotic" else 1e-3)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("method", ["classic+nl-fast", "hs-brightness"])
+def test_rubberwhale(golden, rubberwhale, method):
+    """The north-star parity target: |dAEPE| <= 1e-3 vs the NumPy reference on
+    RubberWhale; |dAAE| <= 0.02 deg; mean EPE to the reference uv <= 5e-3 px,
+    median <= 1e-3, p99 <= 0.05."""
+    import optical_flow
+    from optical_flow.evaluation.metrics import flow_angular_error as fae
+    im1, im2, gt = rubberwhale
+    ref = golden("rubberwhale_ref.npz")[method].astype(np.float64)
+    uv = optical_flow.estimate_flow(im1, im2, method)
+    a_gpu = fae(gt[..., 0], gt[..., 1], uv[..., 0], uv[..., 1])
+    a_ref = fae(gt[..., 0], gt[..., 1], ref[..., 0], ref[..., 1])
+    s = epe_stats(uv, ref)
+    print(method, "gpu AAE/AEPE", a_gpu[0], a_gpu[2], "ref", a_ref[0], a_ref[2], s)
+    assert abs(a_gpu[2] - a_ref[2]) <= 1e-3
+    assert abs(a_gpu[0] - a_ref[0]) <= 0.02
+    assert s["mean"] <= 5e-3 and s["median"] <= 1e-3 and s["p99"] <= 0.05, s
