@@ -1,0 +1,265 @@
+"""Benchmark: image pairs/s for Classic+NL-fast on 1920x1080 synthetic pairs
+(BASELINE.json metric; SURVEY.md §8d config 4, and config 5 across GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One process per GPU.  A step = every rank runs estimate_flow on its P
+device-resident pairs (inputs uploaded to HBM before timing: RGB -> gray/Lab,
+ROF, pyramids, GNC x levels x IRLS, all on the GPU) and, for N > 1, the flows
+are gathered to rank 0 with RCCL over xGMI.  Timed region: barrier +
+device sync on both sides, max over ranks.  value = pairs processed by all
+ranks / time (weak scaling: P pairs per GPU).
+
+Also reported (one JSON line on rank 0):
+  roofline      dominant HBM kernel: algorithmic bytes per launch / mean
+                HIP-event duration of that kernel over a profiled replay of
+                the timed steps; peak 8 TB/s; traffic from profiles/ PMC if
+                present (else null)
+  cpu_baseline  the float64 C oracle (oracle/, OpenMP) on a bounded crop of
+                the same pair, scaled by pixel count to pairs/s
+  ms_per_level  GPU time of each compute_flow_base (coarse -> fine, per stage)
+  aepe_gt       accuracy against the analytic ground truth
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "optical-flow-python_amd"))
+
+import numpy as np  # noqa: E402
+
+from optical_flow import _abi, _native  # noqa: E402  (loads liboptflow.so before torch)
+from optical_flow.methods.config import load_of_method  # noqa: E402
+from optical_flow.utils.synthetic import synth_pair  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# algorithmic bytes per pixel of each kernel's compulsory I/O (DESIGN.md
+# "Kernels and rooflines"); fp32 = 4 B, float2 = 8 B, planes counted once
+KERNEL_BYTES_PER_PX = {
+    "pcg_spmv": 8 + 8 + 28 + 8 + 8,        # z, p_old, 7 coef planes -> p, q
+    "pcg_update": 32 + 12 + 24,            # x, r, p, q, a_uu/a_uv/a_vv -> x, r, z
+    "flow_operator": 8 + 12 + 28 + 8,      # uv, It/Ix/Iy -> 7 coef + rhs
+    "partial_deriv_hermite": 8 + 4 * 4 + 3 * 4 + 12,  # uv, I2/DX/DY/DXY, I1/I1x/I1y -> It/Ix/Iy
+    "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ
+    "wmf": 8 + 4 + 12 + 8,                 # uv, occ, Lab -> uv
+    "rof_iter": 4 + 8 + 8,                 # im, p -> p (per channel)
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pairs", type=int, default=1, help="pairs per GPU per step")
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--method", default="classic+nl-fast")
+    ap.add_argument("--solver", default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=180, help="crop height of the CPU-baseline sample")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist  # gloo only: barrier, max-reduce, RCCL id exchange
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return dist, world, rank, local
+    return None, 1, 0, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_seeds(rank, pairs):
+    """Pair k of the global batch uses seed k; rank r owns [r*P, (r+1)*P)."""
+    return [rank * pairs + k for k in range(pairs)]
+
+
+def make_params(args):
+    ope = load_of_method(args.method)
+    if args.solver:
+        ope.solver = args.solver
+    P = ope.to_params()
+    P.guide_mode = int(ope._METHOD == "classic_nl" and ope.color_images is not None)
+    P.display = 0
+    return P
+
+
+def run_step(ctx, P0, nslots, stats=None):
+    for s in range(nslots):
+        P = _abi.OfParams()
+        C.memmove(C.byref(P), C.byref(P0), C.sizeof(P0))  # alpha is updated per call
+        ctx.check(ctx.lib.of_pair_run(ctx.handle, s, C.byref(P), None if stats is None else C.byref(stats)))
+
+
+def cpu_baseline(args):
+    """float64 oracle on a bounded crop of pair 0, scaled by pixel count."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / baseline only
+    h = min(args.cpu_sample, args.height)
+    w = int(round(h * args.width / args.height))
+    im1, im2, _ = synth_pair(args.height, args.width, 0)
+    y0, x0 = (args.height - h) // 2, (args.width - w) // 2
+    a, b = im1[y0:y0 + h, x0:x0 + w], im2[y0:y0 + h, x0:x0 + w]
+    t0 = time.perf_counter()
+    oracle.estimate_flow(a, b, args.method, solver=args.solver)
+    dt = time.perf_counter() - t0
+    scale = (args.height * args.width) / (h * w)
+    return {"value": 1.0 / (dt * scale), "unit": "pairs/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"float64 C oracle (OpenMP) estimate_flow('{args.method}') on a {h}x{w} centre crop of "
+                      f"synth_pair({args.height},{args.width},0): {dt:.2f} s, scaled x{scale:.1f} by pixel count"}
+
+
+def load_pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, written by profiles/collect.sh)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    dist, world, rank, local = dist_setup(args)
+    ctx = _native.Context(local)
+    lib = ctx.lib
+    H, W = args.height, args.width
+    P0 = make_params(args)
+
+    # inputs resident in HBM before timing
+    seeds = shard_seeds(rank, args.pairs)
+    gts = []
+    for s, seed in enumerate(seeds):
+        im1, im2, gt = synth_pair(H, W, seed)
+        gts.append(gt)
+        a1, a2 = _native.f32(im1), _native.f32(im2)
+        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(a1), _native.ptr(a2), H, W, 3))
+    if world > 1:
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            ctx.check(lib.of_rccl_unique_id(uid))
+        obj = [bytes(uid.raw)]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.check(lib.of_rccl_init(ctx.handle, obj[0], world, rank))
+
+    def step():
+        run_step(ctx, P0, args.pairs)
+        if world > 1:
+            ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
+
+    for _ in range(args.warmup):
+        step()
+    barrier(dist)
+    ctx.check(lib.of_synchronize(ctx.handle))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.check(lib.of_synchronize(ctx.handle))
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    value = world * args.pairs * args.steps / elapsed
+
+    # per-level times + accuracy from one more (untimed) pair
+    st = _abi.OfStats()
+    P = _abi.OfParams()
+    C.memmove(C.byref(P), C.byref(P0), C.sizeof(P0))
+    ctx.check(lib.of_pair_run(ctx.handle, 0, C.byref(P), C.byref(st)))
+    uv = np.empty((2, H, W), dtype=np.float32)
+    ctx.check(lib.of_pair_download(ctx.handle, 0, _native.ptr(uv)))
+    uv = np.moveaxis(uv, 0, 2)
+    aepe = float(np.sqrt(((uv - gts[0]) ** 2).sum(-1)).mean())
+    sd = st.as_dict()
+
+    roofline = None
+    ktimes = {}
+    if not args.no_profile:
+        # profiled replay of the timed steps: HIP events around every launch
+        # on the ctx stream (the stream the kernels run on)
+        ctx.check(lib.of_set_profiling(ctx.handle, 1))
+        for _ in range(args.steps):
+            run_step(ctx, P0, args.pairs)
+        n = C.c_int(0)
+        names = (C.c_char_p * 256)()
+        ms = (C.c_double * 256)()
+        cnt = (C.c_int64 * 256)()
+        pxs = (C.c_double * 256)()
+        ctx.check(lib.of_kernel_times(ctx.handle, 256, names, ms, cnt, pxs, C.byref(n)))
+        ctx.check(lib.of_set_profiling(ctx.handle, 0))
+        for i in range(n.value):
+            ktimes[names[i].decode()] = {"ms_total": ms[i] / args.steps, "launches": int(cnt[i]) / args.steps,
+                                         "px": pxs[i] / args.steps}
+        hbm = {k: v for k, v in ktimes.items() if k in KERNEL_BYTES_PER_PX}
+        if hbm:
+            dom = max(hbm, key=lambda k: hbm[k]["ms_total"])
+            # algorithmic bytes per launch = bytes/px x pixels of the level the
+            # launch ran on (exact per-launch pixel counts from the library)
+            px_per_launch = hbm[dom]["px"] / hbm[dom]["launches"]
+            avg_ms = hbm[dom]["ms_total"] / hbm[dom]["launches"]
+            bytes_per_launch = KERNEL_BYTES_PER_PX[dom] * px_per_launch
+            ach = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": load_pmc_traffic(dom),
+                        "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": round(avg_ms, 5),
+                        "px_per_launch": int(px_per_launch)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": "image-pairs/sec at 1920x1080 Classic+NL-fast (+ ms/pyramid-level, AEPE)",
+            "value": round(value, 4), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.method} on synth_pair({H},{W},seed) RGB, {args.pairs} pair(s)/GPU/step",
+                       "method": args.method, "height": H, "width": W, "pairs_per_gpu": args.pairs,
+                       "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
+                       "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
+            "roofline": roofline, "cpu_baseline": cpu,
+            "ms_per_level": [{"stage": l["stage"], "h": l["h"], "w": l["w"], "ms": round(l["ms"], 3)}
+                             for l in sd["levels"]],
+            "aepe_gt": round(aepe, 5), "solver_iters_total": sd["solver_iters_total"],
+            "solver_iters_max": sd["solver_iters_max"], "solves": sd["solves"],
+            "kernel_ms_per_pair": {k: round(v["ms_total"] / args.pairs, 3) for k, v in
+                                   sorted(ktimes.items(), key=lambda kv: -kv[1]["ms_total"])[:12]},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        lib.of_rccl_finalize(ctx.handle)
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

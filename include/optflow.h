@@ -143,8 +143,10 @@ const char *of_last_error(of_ctx *ctx);
 int of_synchronize(of_ctx *ctx);
 /* per-kernel HIP-event timing on the ctx stream (0 = off); see of_kernel_times */
 int of_set_profiling(of_ctx *ctx, int enable);
-/* kernel timing accumulated since enable: names[i] (static strings), ms[i], count[i] */
-int of_kernel_times(of_ctx *ctx, int max, const char **names, double *ms, int64_t *count, int *n);
+/* kernel timing accumulated since enable: per kernel name total ms, launch
+ * count and pixels processed (sum over launches of the level's H*W; ROF
+ * counts H*W*channels); any output pointer may be NULL */
+int of_kernel_times(of_ctx *ctx, int max, const char **names, double *ms, int64_t *count, double *pixels, int *n);
 
 /*
  * Whole pair: estimate_flow (optical_flow/interface.py:11-71) without its

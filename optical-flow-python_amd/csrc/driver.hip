@@ -85,6 +85,11 @@ struct F2 {  // pitched float2 field
 struct ProfRec {
   const char *name;
   hipEvent_t e0, e1;
+  double px;
+};
+struct KTime {
+  double ms = 0, px = 0;
+  int64_t n = 0;
 };
 
 struct Slot {
@@ -112,7 +117,8 @@ struct of_ctx {
   std::vector<hipEvent_t> tev_pool;  // level timing events, recycled per API call
   size_t tev_used = 0;
   std::vector<ProfRec> pending;
-  std::map<std::string, std::pair<double, int64_t>> ktimes;
+  std::map<std::string, KTime> ktimes;
+  double cur_px = 0;  // pixels processed by the launches being issued (profiling)
   std::vector<Slot> slots;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -147,8 +153,9 @@ void flush_prof(of_ctx *c) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
     auto &s = c->ktimes[r.name];
-    s.first += ms;
-    s.second += 1;
+    s.ms += ms;
+    s.px += r.px;
+    s.n += 1;
   }
   c->pending.clear();
   c->ev_used = 0;
@@ -168,7 +175,7 @@ void launch(of_ctx *c, const char *name, K kernel, dim3 g, dim3 b, size_t shm, A
   HIPCHK(hipGetLastError());
   if (c->prof) {
     HIPCHK(hipEventRecord(e1, c->stream));
-    c->pending.push_back({name, e0, e1});
+    c->pending.push_back({name, e0, e1, c->cur_px});
   }
 }
 
@@ -313,6 +320,7 @@ std::vector<Img> build_pyramid(of_ctx *c, const Img &img, int levels, double spa
 
 // structure_texture_decomposition_rof (image_processing.py:52-136) on all planes
 Img rof_texture(of_ctx *c, const Img &in, double theta, int iters, double alp) {
+  c->cur_px = (double)in.H * in.W * in.C;
   Img nrm = new_img(c, in.H, in.W, in.C);
   copy_img(c, nrm, in);
   scale_img(c, nrm, -1.0f, 1.0f, 0);
@@ -442,80 +450,107 @@ struct SolveResult {
   double rel;
 };
 
-SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
-  const int H = b.H, W = b.W;
-  Grid2 g = grid2(H, W, MAX_RED_BLOCKS);
-  const size_t ps = coef.ps();
-  const int solver = P->solver;
-  int maxiter;
-  if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
-    const bool block = solver == OF_SOLVER_BACKSLASH;
-    const double rtol = block ? P->exact_rtol : P->pcg_rtol;
-    maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
-    F2 r = new_f2(c, H, W), z = new_f2(c, H, W), pa = new_f2(c, H, W), pb = new_f2(c, H, W), q = new_f2(c, H, W);
-    if (block)
-      launch(c, "pcg_init", k_pcg_init<true>, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p,
-             r.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter, rtol, maxiter);
-    else
-      launch(c, "pcg_init", k_pcg_init<false>, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p,
-             r.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter, rtol, maxiter);
-    int enq = 0, chunk = 8, nchunks = 0;
-    F2 pold = pa, pnew = pb;
-    while (true) {
-      int n = std::min(chunk, maxiter - enq);
-      for (int t = 0; t < n; ++t) {
-        launch(c, "pcg_spmv", k_pcg_dir_spmv, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)z.p,
-               (const float2 *)pold.p, pnew.p, q.p, H, W, b.P, ps, c->d_state, c->d_partials, c->d_counter);
-        if (block)
-          launch(c, "pcg_update", k_pcg_update<true>, g.grid, g.block, 0, (const float *)coef.p, x.p, r.p,
-                 (const float2 *)pnew.p, (const float2 *)q.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials,
-                 c->d_counter);
-        else
-          launch(c, "pcg_update", k_pcg_update<false>, g.grid, g.block, 0, (const float *)coef.p, x.p, r.p,
-                 (const float2 *)pnew.p, (const float2 *)q.p, z.p, H, W, b.P, ps, c->d_state, c->d_partials,
-                 c->d_counter);
-        std::swap(pold, pnew);
-      }
-      enq += n;
-      const int slot = nchunks & 1;
-      HIPCHK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipEventRecord(c->ev_state[slot], c->stream));
-      ++nchunks;
-      if (enq >= maxiter) break;
-      if (nchunks >= 2) {  // check the previous chunk while this one runs
-        HIPCHK(hipEventSynchronize(c->ev_state[slot ^ 1]));
-        if (c->h_state[slot ^ 1].done) break;
-      }
-      chunk = std::min(chunk * 2, 64);
-    }
-    HIPCHK(hipEventSynchronize(c->ev_state[(nchunks - 1) & 1]));
-    const PcgState &s = c->h_state[(nchunks - 1) & 1];
-    return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
-  }
-  // red-black block SOR
-  maxiter = P->sor_max_iters;
-  launch(c, "sor_init", k_sor_init, g.grid, g.block, 0, x.p, H, W, b.P, c->d_state, maxiter);
-  int enq = 0, chunk = 16, nchunks = 0;
-  while (true) {
-    int n = std::min(chunk, maxiter - enq);
-    for (int t = 0; t < n; ++t)
-      for (int color = 0; color < 2; ++color)
-        launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, (const float *)coef.p, (const float2 *)b.p, x.p, H, W,
-               b.P, ps, color, (float)P->sor_omega, (float)P->sor_tol, c->d_state, c->d_partials, c->d_counter);
+// grid for the 2-pixels-per-thread solver kernels, <= PCG_MAX_BLOCKS blocks
+Grid2 pair_grid(int H, int W) {
+  Grid2 g;
+  g.block = dim3(OF_BX, OF_BY, 1);
+  int gx = (W + 2 * OF_BX - 1) / (2 * OF_BX), gy = (H + OF_BY - 1) / OF_BY;
+  int cap = std::max(1, PCG_MAX_BLOCKS / gx);
+  g.grid = dim3(gx, std::min(gy, cap), 1);
+  g.nblocks = g.grid.x * g.grid.y;
+  return g;
+}
+
+// enqueue iterations in growing chunks; check the previous chunk's state
+// (pinned, double-buffered) while the current one runs
+template <typename Enq>
+int run_chunked(of_ctx *c, int maxiter, int first_chunk, int max_chunk, Enq enqueue_iter) {
+  int enq = 0, chunk = first_chunk, nchunks = 0;
+  while (enq < maxiter) {
+    const int n = std::min(chunk, maxiter - enq);
+    for (int t = 0; t < n; ++t) enqueue_iter(enq + t);
     enq += n;
     const int slot = nchunks & 1;
     HIPCHK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipEventRecord(c->ev_state[slot], c->stream));
     ++nchunks;
-    if (enq >= maxiter) break;
     if (nchunks >= 2) {
       HIPCHK(hipEventSynchronize(c->ev_state[slot ^ 1]));
       if (c->h_state[slot ^ 1].done) break;
     }
-    chunk = std::min(chunk * 2, 128);
+    chunk = std::min(chunk * 2, max_chunk);
   }
-  HIPCHK(hipEventSynchronize(c->ev_state[(nchunks - 1) & 1]));
-  const PcgState &s = c->h_state[(nchunks - 1) & 1];
+  return enq;
+}
+
+SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+  const int H = b.H, W = b.W;
+  c->cur_px = (double)H * W;
+  const size_t ps = coef.ps();
+  const int solver = P->solver;
+  if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
+    const bool block = solver == OF_SOLVER_BACKSLASH;
+    Grid2 g = pair_grid(H, W);
+    PcgArgs a;
+    a.coef = coef.p;
+    a.x = x.p;
+    a.b = b.p;
+    F2 r = new_f2(c, H, W), z = new_f2(c, H, W), pa = new_f2(c, H, W), pb = new_f2(c, H, W), q = new_f2(c, H, W);
+    a.r = r.p;
+    a.z = z.p;
+    a.q = q.p;
+    a.H = H;
+    a.W = W;
+    a.P = b.P;
+    a.ps = ps;
+    a.nb = g.nblocks;
+    a.part = c->d_partials;
+    a.st = c->d_state;
+    a.rtol = block ? P->exact_rtol : P->pcg_rtol;
+    a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
+    a.p_old = pa.p;
+    a.p_new = pb.p;
+    if (block) launch(c, "pcg_init", k_pcg_init<true>, g.grid, g.block, 0, a);
+    else launch(c, "pcg_init", k_pcg_init<false>, g.grid, g.block, 0, a);
+    const int enq = run_chunked(c, a.maxiter, 8, 32, [&](int k) {
+      PcgArgs ak = a;
+      ak.p_old = (k & 1) ? pb.p : pa.p;
+      ak.p_new = (k & 1) ? pa.p : pb.p;
+      launch(c, "pcg_spmv", k_pcg_dir_spmv, g.grid, g.block, 0, ak, k);
+      if (block) launch(c, "pcg_update", k_pcg_update<true>, g.grid, g.block, 0, ak, k);
+      else launch(c, "pcg_update", k_pcg_update<false>, g.grid, g.block, 0, ak, k);
+    });
+    launch(c, "pcg_final", k_pcg_final, dim3(1), dim3(OF_BX, OF_BY), 0, a, enq);
+    HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const PcgState &s = c->h_state[0];
+    return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
+  }
+  // red-black block SOR
+  Grid2 g = grid2(H, W, PCG_MAX_BLOCKS);
+  SorArgs a;
+  a.coef = coef.p;
+  a.b = b.p;
+  a.x = x.p;
+  a.H = H;
+  a.W = W;
+  a.P = b.P;
+  a.ps = ps;
+  a.nb = g.nblocks;
+  a.part = c->d_partials;
+  a.st = c->d_state;
+  a.omega = (float)P->sor_omega;
+  a.tol = (float)P->sor_tol;
+  a.maxiter = P->sor_max_iters;
+  launch(c, "sor_init", k_sor_init, g.grid, g.block, 0, a);
+  const int enq = run_chunked(c, a.maxiter, 16, 64, [&](int k) {
+    launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 0, k);
+    launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 1, k);
+  });
+  launch(c, "sor_final", k_sor_final, dim3(1), dim3(OF_BX, OF_BY), 0, a, enq);
+  HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const PcgState &s = c->h_state[0];
   return {s.iter, s.done, 0.0};
 }
 
@@ -528,8 +563,9 @@ void note_solve(of_stats *st, const SolveResult &r) {
 }
 
 double norm2(of_ctx *c, const F2 &x) {
-  Grid2 g = grid2(x.H, x.W, MAX_RED_BLOCKS);
-  launch(c, "norm2", k_norm2, g.grid, g.block, 0, (const float2 *)x.p, x.H, x.W, x.P, c->d_partials, c->d_counter,
+  Grid2 g = grid2(x.H, x.W, PCG_MAX_BLOCKS);
+  launch(c, "norm2", k_norm2_part, g.grid, g.block, 0, (const float2 *)x.p, x.H, x.W, x.P, c->d_partials);
+  launch(c, "norm2", k_norm2_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_partials, g.nblocks,
          c->d_norm);
   HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -581,6 +617,7 @@ struct LevelIn {
 // HSOpticalFlow.compute_flow_base (hs.py:109-142)
 void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  c->cur_px = (double)H * W;
   LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, 0.5);
   Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
   Img coef = new_img(c, H, W, 7);
@@ -591,6 +628,7 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
     note_solve(st, solve(c, P, coef, rhs, x));
+    c->cur_px = (double)H * W;
     if (std::sqrt(norm2(c, x)) < 1e-3) break;
     launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)x.p, P->limit_update, H, W, uv.P);
     if (P->median_filter_size)
@@ -606,6 +644,7 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
 void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double alpha, int max_linear,
                of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  c->cur_px = (double)H * W;
   const double blend = P->method == OF_METHOD_BA ? P->blend : 0.5;  // classic_nl.py:232 passes no blend
   LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, blend);
   Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
@@ -621,6 +660,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
     for (int jl = 0; jl < max_linear; ++jl) {
       flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
       note_solve(st, solve(c, P, coef, rhs, x));
+      c->cur_px = (double)H * W;
       const bool filt = P->median_filter_size != 0;
       launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
              (const float2 *)uv.p, (const float2 *)x.p, P->limit_update, uv1.p, (const float *)L.im.p,
@@ -645,6 +685,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
 void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvhat, double alpha, bool replacement,
                 of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
+  c->cur_px = (double)H * W;
   LevelDeriv D = level_deriv(c, L.im, nc, P->interp, P->deriv_filter, 0.5);
   Img It = new_img(c, H, W, nc), Ix = new_img(c, H, W, nc), Iy = new_img(c, H, W, nc);
   Img coef = new_img(c, H, W, 7);
@@ -663,6 +704,7 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
     for (int jl = 0; jl < P->max_linear; ++jl) {
       flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
       note_solve(st, solve(c, P, coef, rhs, x));
+      c->cur_px = (double)H * W;
       // duv = clip(x): computed as (0 + clip(x))
       HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
       launch(c, "add_update", k_add_update, g.grid, g.block, 0, duv.p, (const float2 *)x.p, P->limit_update, H, W,
@@ -899,7 +941,7 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 4 * MAX_RED_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 4 * PCG_MAX_BLOCKS));
     HIPCHK(hipMalloc(&c->d_counter, sizeof(unsigned) * 16));
     HIPCHK(hipMemset(c->d_counter, 0, sizeof(unsigned) * 16));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
@@ -960,14 +1002,15 @@ int of_set_profiling(of_ctx *c, int enable) {
   return OF_OK;
 }
 
-int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t *count, int *n) {
+int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t *count, double *pixels, int *n) {
   if (!c || !n) return OF_EINVAL;
   int k = 0;
   for (auto &kv : c->ktimes) {
     if (k < max) {
       if (names) names[k] = kv.first.c_str();
-      if (ms) ms[k] = kv.second.first;
-      if (count) count[k] = kv.second.second;
+      if (ms) ms[k] = kv.second.ms;
+      if (count) count[k] = kv.second.n;
+      if (pixels) pixels[k] = kv.second.px;
     }
     ++k;
   }

@@ -39,8 +39,7 @@ struct DerivArgs {
 
 // PCG scalar state (device-resident; mirrored to pinned host memory)
 struct PcgState {
-  double rho;       // r.z of the current iterate
-  double pq;
+  double rho[2];    // r.z of iterate k at rho[k & 1]
   double rr;        // r.r
   double atol;      // rtol * ||b||
   double bnorm;

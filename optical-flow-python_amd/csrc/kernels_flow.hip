@@ -290,28 +290,6 @@ __global__ void k_sub2(const float2 *__restrict__ a, const float2 *__restrict__ 
   }
 }
 
-// sum of squares of a float2 field (HS early exit ||x||_2 < 1e-3, hs.py:127)
-__global__ void k_norm2(const float2 *__restrict__ x, int H, int W, int P, double *partials, unsigned *counter,
-                        double *result) {
-  __shared__ double lds[16];
-  double v[1] = {0.0};
-  OF_FOR_PIXELS(H, W) {
-    if (j >= W) continue;
-    float2 a = x[(size_t)i * P + j];
-    v[0] += (double)a.x * a.x + (double)a.y * a.y;
-  }
-  block_sum<1>(v, lds);
-  const int nb = gridDim.x * gridDim.y;
-  if (arrive_last<1>(v, partials, counter, nb, blockIdx.x + blockIdx.y * gridDim.x)) {
-    double s[1];
-    final_sum<1>(s, partials, nb, lds);
-    if (threadIdx.x == 0 && threadIdx.y == 0) {
-      *result = s[0];
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // scipy.ndimage.median_filter(size=S, mode='reflect'): rank selection with
 // index tie-break (the element of rank S*S/2), branch-free.

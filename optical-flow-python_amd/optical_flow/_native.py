@@ -32,7 +32,7 @@ _SIGS = {
     "of_last_error": ([_vp], C.c_char_p),
     "of_synchronize": ([_vp], C.c_int),
     "of_set_profiling": ([_vp, C.c_int], C.c_int),
-    "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _ip], C.c_int),
+    "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _dp, _ip], C.c_int),
     "of_estimate_flow": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, C.c_int, _fp, _fp,
                           C.POINTER(OfStats)], C.c_int),
     "of_compute_flow": ([_vp, C.POINTER(OfParams), _fp, C.c_int, C.c_int, C.c_int, _fp, C.c_int, _fp, _fp,
