@@ -42,8 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # algorithmic bytes per pixel of each kernel's compulsory I/O (DESIGN.md
 # "Kernels and rooflines"); fp32 = 4 B, float2 = 8 B, planes counted once
 KERNEL_BYTES_PER_PX = {
-    "pcg_spmv": 8 + 8 + 28 + 8 + 8,        # z, p_old, 7 coef planes -> p, q
-    "pcg_update": 32 + 12 + 24,            # x, r, p, q, a_uu/a_uv/a_vv -> x, r, z
+    "pcg_iter": 4 * 8 + 28 + 4 * 8,        # fused CG iteration: r, q, p, x + 7 coef planes -> r, p, q, x
     "flow_operator": 8 + 12 + 28 + 8,      # uv, It/Ix/Iy -> 7 coef + rhs
     "partial_deriv_hermite": 8 + 4 * 4 + 3 * 4 + 12,  # uv, I2/DX/DY/DXY, I1/I1x/I1y -> It/Ix/Iy
     "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ

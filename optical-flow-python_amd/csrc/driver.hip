@@ -490,37 +490,52 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
   const int solver = P->solver;
   if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
     const bool block = solver == OF_SOLVER_BACKSLASH;
-    Grid2 g = pair_grid(H, W);
+    // fused-iteration geometry: 128-column strips x bands of R rows, 4 bands
+    // per block, <= PCG_MAX_BLOCKS blocks, ~2048 waves when the level allows
+    const int nstrips = (W + 127) / 128;
+    int nbands = std::max(1, std::min((H + 3) / 4, 2048 / nstrips));
+    int R = (H + nbands - 1) / nbands;
+    nbands = (H + R - 1) / R;
+    int gyb = (nbands + 3) / 4;
+    while (nstrips * gyb > PCG_MAX_BLOCKS) {
+      ++R;
+      nbands = (H + R - 1) / R;
+      gyb = (nbands + 3) / 4;
+    }
+    dim3 grid(nstrips, gyb), blk(OF_BX, OF_BY);
     PcgArgs a;
+    memset(&a, 0, sizeof(a));
     a.coef = coef.p;
     a.x = x.p;
     a.b = b.p;
-    F2 r = new_f2(c, H, W), z = new_f2(c, H, W), pa = new_f2(c, H, W), pb = new_f2(c, H, W), q = new_f2(c, H, W);
-    a.r = r.p;
-    a.z = z.p;
-    a.q = q.p;
+    F2 rb[2] = {new_f2(c, H, W), new_f2(c, H, W)}, qb[2] = {new_f2(c, H, W), new_f2(c, H, W)},
+       pb[2] = {new_f2(c, H, W), new_f2(c, H, W)};
     a.H = H;
     a.W = W;
     a.P = b.P;
     a.ps = ps;
-    a.nb = g.nblocks;
+    a.nb = nstrips * gyb;
     a.part = c->d_partials;
     a.st = c->d_state;
     a.rtol = block ? P->exact_rtol : P->pcg_rtol;
     a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
-    a.p_old = pa.p;
-    a.p_new = pb.p;
-    if (block) launch(c, "pcg_init", k_pcg_init<true>, g.grid, g.block, 0, a);
-    else launch(c, "pcg_init", k_pcg_init<false>, g.grid, g.block, 0, a);
-    const int enq = run_chunked(c, a.maxiter, 8, 32, [&](int k) {
+    HIPCHK(hipMemsetAsync(c->d_state, 0, sizeof(PcgState), c->stream));
+    auto args_k = [&](int k) {
       PcgArgs ak = a;
-      ak.p_old = (k & 1) ? pb.p : pa.p;
-      ak.p_new = (k & 1) ? pa.p : pb.p;
-      launch(c, "pcg_spmv", k_pcg_dir_spmv, g.grid, g.block, 0, ak, k);
-      if (block) launch(c, "pcg_update", k_pcg_update<true>, g.grid, g.block, 0, ak, k);
-      else launch(c, "pcg_update", k_pcg_update<false>, g.grid, g.block, 0, ak, k);
+      const int cur = k & 1, prev = cur ^ 1;
+      ak.r_in = rb[prev].p;
+      ak.q_in = qb[prev].p;
+      ak.p_old = pb[prev].p;
+      ak.r_out = rb[cur].p;
+      ak.q_out = qb[cur].p;
+      ak.p_new = pb[cur].p;
+      return ak;
+    };
+    const int enq = run_chunked(c, a.maxiter + 1, 8, 32, [&](int k) {
+      if (block) launch(c, "pcg_iter", k_pcg_iter<true>, grid, blk, 0, args_k(k), k, R, nbands);
+      else launch(c, "pcg_iter", k_pcg_iter<false>, grid, blk, 0, args_k(k), k, R, nbands);
     });
-    launch(c, "pcg_final", k_pcg_final, dim3(1), dim3(OF_BX, OF_BY), 0, a, enq);
+    launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
     HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const PcgState &s = c->h_state[0];
@@ -941,7 +956,7 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 4 * PCG_MAX_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 8 * PCG_MAX_BLOCKS));
     HIPCHK(hipMalloc(&c->d_counter, sizeof(unsigned) * 16));
     HIPCHK(hipMemset(c->d_counter, 0, sizeof(unsigned) * 16));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));

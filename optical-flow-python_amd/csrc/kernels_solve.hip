@@ -89,11 +89,13 @@ __device__ __forceinline__ void write_partials(double (&v)[NV], double *part, do
 struct PcgArgs {
   const float *coef;  // 7 planes, plane stride ps
   float2 *x, *r, *z, *p_old, *p_new, *q;
+  const float2 *r_in, *q_in;  // fused iteration: iterate k-1
+  float2 *r_out, *q_out;      // fused iteration: iterate k
   const float2 *b;
   int H, W, P;
   size_t ps;
   int nb;  // blocks of this grid (== blocks of every launch of the solve)
-  double *part;  // [3][PCG_MAX_BLOCKS]: 0 = p.q, 1 = r.z, 2 = r.r
+  double *part;  // [5][PCG_MAX_BLOCKS] partial sums (layout per kernel pair)
   PcgState *st;
   double rtol;
   int maxiter;
@@ -247,6 +249,197 @@ __global__ __launch_bounds__(256) void k_pcg_final(PcgArgs a, int k) {
     a.st->rr = sums[1];
     a.st->iter = k;
     a.st->done = sqrt(sums[1]) < a.st->atol ? 1 : 2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused CG iteration: one launch per iteration (k_pcg_iter).  Launch K_k
+//   r_k = r_{k-1} - alpha_{k-1} q_{k-1},  x_k = x_{k-1} + alpha_{k-1} p_{k-1},
+//   z_k = M^-1 r_k,  p_k = z_k + beta_k p_{k-1},  q_k = A p_k
+// and per-block sums S = (p.q, q.z, q.M^-1 q, r.z, r.r) of iterate k.  The
+// prologue of K_{k+1} turns the sums of K_k into
+//   alpha_k = (r.z)_k / (p.q)_k,  rho_{k+1} = (r.z)_k - 2 alpha_k (q.z)_k
+//   + alpha_k^2 (q.M^-1 q)_k (exact CG algebra), beta_{k+1} = rho_{k+1}/(r.z)_k
+// and applies scipy's test ||r_k|| < rtol ||b|| before iteration k.
+//
+// Geometry: a wave owns a 128-column strip (2 px per lane) and sweeps a band
+// of R rows top to bottom with a 3-row window in registers, so r, z, p of
+// every pixel are formed once; left/right neighbours come from the adjacent
+// lanes (DPP/bpermute), only lanes 0 and 63 reload the pixel across the
+// strip edge.  A block = 4 waves = 4 consecutive bands of one strip.
+struct PixIn {  // what a row load produces for one pixel
+  float2 r, z, p, pold;
+  float a, c, d;
+};
+
+template <bool BLOCK>
+__device__ __forceinline__ PixIn load_pix(const PcgArgs &g, int k, float alpha, float beta, size_t kk) {
+  PixIn v;
+  v.a = g.coef[4 * g.ps + kk];
+  v.c = g.coef[5 * g.ps + kk];
+  v.d = g.coef[6 * g.ps + kk];
+  if (k == 0) {
+    v.r = g.b[kk];
+    v.pold = make_float2(0.f, 0.f);
+  } else {
+    const float2 ro = g.r_in[kk], qo = g.q_in[kk];
+    v.r = make_float2(ro.x - alpha * qo.x, ro.y - alpha * qo.y);
+    v.pold = g.p_old[kk];
+  }
+  v.z = precond<BLOCK>(v.a, v.c, v.d, v.r);
+  v.p = k == 0 ? v.z : make_float2(v.z.x + beta * v.pold.x, v.z.y + beta * v.pold.y);
+  return v;
+}
+
+__device__ __forceinline__ float shfl_up1(float v) { return __shfl_up(v, 1, 64); }
+__device__ __forceinline__ float shfl_dn1(float v) { return __shfl_down(v, 1, 64); }
+
+// the shared prologue: returns 1 when the solve is finished (state written)
+__device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds, float *alpha, float *beta) {
+  __shared__ int s_exit;
+  __shared__ float s_ab[2];
+  double S[5];
+  prologue_sum<5>(S, g.part, g.nb, lds);  // of K_{k-1}: pq, qz, qMq, rz, rr
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+    const double rn = sqrt(S[4]);
+    const double atol = k == 1 ? g.rtol * rn : g.st->atol;
+    int done = 0;
+    if (k == 1 && S[4] == 0.0) done = 3;
+    else if (rn < atol) done = 1;
+    else if (k - 1 >= g.maxiter) done = 2;
+    const double al = S[3] / S[0];
+    const double rho = S[3] - 2.0 * al * S[1] + al * al * S[2];
+    if (lead) {
+      if (k == 1) { g.st->bnorm = rn; g.st->atol = atol; }
+      g.st->iter = k - 1;
+      g.st->rr = S[4];
+      g.st->rho[k & 1] = rho;
+      if (done) g.st->done = done;
+    }
+    s_exit = done;
+    s_ab[0] = (float)al;
+    s_ab[1] = (float)(rho / S[3]);
+  }
+  __syncthreads();
+  *alpha = s_ab[0];
+  *beta = s_ab[1];
+  return s_exit;
+}
+
+template <bool BLOCK>
+__global__ __launch_bounds__(256) void k_pcg_iter(PcgArgs g, int k, int R, int nbands) {
+  __shared__ double lds[64];
+  if (g.st->done) return;
+  float alpha = 0.f, beta = 0.f;
+  if (k >= 1 && pcg_prologue(g, k, lds, &alpha, &beta)) return;
+  if (k == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
+    g.st->iter = 0;
+    g.st->maxiter = g.maxiter;
+  }
+  const int H = g.H, W = g.W, P = g.P;
+  const int lane = threadIdx.x, band = blockIdx.y * 4 + threadIdx.y;
+  const int j0 = blockIdx.x * 128 + 2 * lane;
+  const bool v0 = j0 < W, v1 = j0 + 1 < W;
+  const float *wxu = g.coef, *wyu = g.coef + g.ps, *wxv = g.coef + 2 * g.ps, *wyv = g.coef + 3 * g.ps;
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (band < nbands) {
+    const int r0 = band * R, r1 = min(r0 + R, H);
+    auto load_row = [&](int ii, PixIn &e0, PixIn &e1) {
+      const bool ok = ii >= 0 && ii < H;
+      const size_t kk = (size_t)ii * P + j0;
+      if (ok && v0) e0 = load_pix<BLOCK>(g, k, alpha, beta, kk);
+      else e0.p = make_float2(0.f, 0.f);
+      if (ok && v1) e1 = load_pix<BLOCK>(g, k, alpha, beta, kk + 1);
+      else e1.p = make_float2(0.f, 0.f);
+    };
+    auto p_at = [&](int ii, int jj) -> float2 {  // strip-edge neighbour
+      if (jj < 0 || jj >= W) return make_float2(0.f, 0.f);
+      return load_pix<BLOCK>(g, k, alpha, beta, (size_t)ii * P + jj).p;
+    };
+    PixIn m0, m1, c0, c1, n0, n1;
+    load_row(r0 - 1, m0, m1);
+    load_row(r0, c0, c1);
+    float2 wyu_up = make_float2(0.f, 0.f), wyv_up = wyu_up;  // edge weights row i-1 -> i
+    if (r0 > 0) {
+      const size_t ku = (size_t)(r0 - 1) * P + j0;
+      if (v0) { wyu_up.x = wyu[ku]; wyv_up.x = wyv[ku]; }
+      if (v1) { wyu_up.y = wyu[ku + 1]; wyv_up.y = wyv[ku + 1]; }
+    }
+    for (int i = r0; i < r1; ++i) {
+      load_row(i + 1, n0, n1);
+      const size_t kk = (size_t)i * P + j0;
+      // horizontal neighbours of the pair: lane-1's second pixel, lane+1's first
+      float2 L = make_float2(shfl_up1(c1.p.x), shfl_up1(c1.p.y));
+      float2 Rn = make_float2(shfl_dn1(c0.p.x), shfl_dn1(c0.p.y));
+      float wx0u = v0 ? wxu[kk] : 0.f, wx0v = v0 ? wxv[kk] : 0.f;
+      float wx1u = v1 ? wxu[kk + 1] : 0.f, wx1v = v1 ? wxv[kk + 1] : 0.f;
+      float wLu = shfl_up1(wx1u), wLv = shfl_up1(wx1v);
+      if (lane == 0) {
+        L = p_at(i, j0 - 1);
+        wLu = j0 > 0 ? wxu[kk - 1] : 0.f;
+        wLv = j0 > 0 ? wxv[kk - 1] : 0.f;
+      }
+      if (lane == 63) Rn = p_at(i, j0 + 2);
+      float2 wyu_dn = make_float2(0.f, 0.f), wyv_dn = wyu_dn;
+      if (i < H - 1) {
+        if (v0) { wyu_dn.x = wyu[kk]; wyv_dn.x = wyv[kk]; }
+        if (v1) { wyu_dn.y = wyu[kk + 1]; wyv_dn.y = wyv[kk + 1]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool valid = e ? v1 : v0;
+        if (!valid) continue;
+        const int j = j0 + e;
+        const PixIn &c = e ? c1 : c0;
+        const float2 left = e ? c0.p : L, right = e ? Rn : c1.p;
+        const float wl_u = e ? wx0u : wLu, wl_v = e ? wx0v : wLv;
+        const float wr_u = e ? wx1u : wx0u, wr_v = e ? wx1v : wx0v;
+        const float2 up = e ? m1.p : m0.p, dn = e ? n1.p : n0.p;
+        const float wu_u = e ? wyu_up.y : wyu_up.x, wu_v = e ? wyv_up.y : wyv_up.x;
+        const float wd_u = e ? wyu_dn.y : wyu_dn.x, wd_v = e ? wyv_dn.y : wyv_dn.x;
+        float su = 0.f, sv = 0.f;
+        if (j < W - 1) { su += wr_u * right.x; sv += wr_v * right.y; }
+        if (j > 0) { su += wl_u * left.x; sv += wl_v * left.y; }
+        if (i < H - 1) { su += wd_u * dn.x; sv += wd_v * dn.y; }
+        if (i > 0) { su += wu_u * up.x; sv += wu_v * up.y; }
+        const float2 q = make_float2(c.a * c.p.x + c.c * c.p.y - su, c.c * c.p.x + c.d * c.p.y - sv);
+        const size_t kj = kk + e;
+        g.r_out[kj] = c.r;
+        g.p_new[kj] = c.p;
+        g.q_out[kj] = q;
+        if (k == 0) g.x[kj] = make_float2(0.f, 0.f);
+        else {
+          float2 xx = g.x[kj];
+          xx.x += alpha * c.pold.x;
+          xx.y += alpha * c.pold.y;
+          g.x[kj] = xx;
+        }
+        const float2 mq = precond<BLOCK>(c.a, c.c, c.d, q);
+        acc[0] += (double)c.p.x * q.x + (double)c.p.y * q.y;
+        acc[1] += (double)q.x * c.z.x + (double)q.y * c.z.y;
+        acc[2] += (double)q.x * mq.x + (double)q.y * mq.y;
+        acc[3] += (double)c.r.x * c.z.x + (double)c.r.y * c.z.y;
+        acc[4] += (double)c.r.x * c.r.x + (double)c.r.y * c.r.y;
+      }
+      m0 = c0; m1 = c1; c0 = n0; c1 = n1;
+      wyu_up = wyu_dn;
+      wyv_up = wyv_dn;
+    }
+  }
+  write_partials<5>(acc, g.part, lds);
+}
+
+// after the last enqueued iteration: apply the convergence test to the last
+// iterate and record the final state (1 block)
+__global__ __launch_bounds__(256) void k_pcg_check(PcgArgs g, int k) {
+  __shared__ double lds[64];
+  if (g.st->done) return;
+  float a, b;
+  pcg_prologue(g, k, lds, &a, &b);
+  if (threadIdx.x == 0 && threadIdx.y == 0 && !g.st->done) {
+    g.st->iter = k - 1;
+    g.st->done = 2;
   }
 }
 

@@ -1,0 +1,137 @@
+"""Summarise a tools/profile.sh run: per kernel at the finest level, mean
+dispatch duration, HBM bytes (FETCH_SIZE, WRITE_SIZE; KB units), L2 hit rate,
+and the algorithmic-bytes roofline.  Writes <dir>/summary.json and, with
+--traffic, profiles/pmc_traffic.json (read by bench.py).
+
+usage: python tools/prof_summary.py gpurun_out/prof_TAG [--H 1080 --W 1920] [--traffic]
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "")
+    return n
+
+
+def grid_key(r):
+    """total threads of the dispatch (kernel-trace rows carry X/Y/Z, counter rows the product)"""
+    if "Grid_Size" in r:
+        return int(r["Grid_Size"])
+    return int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+
+
+def load_counters(path, counter):
+    """dispatch id -> summed counter value"""
+    out = collections.defaultdict(float)
+    meta = {}
+    if not os.path.exists(path):
+        return out, meta
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        d = int(r["Dispatch_Id"])
+        out[d] += float(r["Counter_Value"])
+        meta[d] = (short(r["Kernel_Name"]), grid_key(r))
+    return out, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--traffic", action="store_true")
+    a = ap.parse_args()
+    import bench  # noqa: E402  (KERNEL_BYTES_PER_PX, profiler names)
+    d = a.dir
+    trace = list(csv.DictReader(open(os.path.join(d, "trace_kernel_trace.csv"))))
+    dur = collections.defaultdict(list)
+    for r in trace:
+        dur[(short(r["Kernel_Name"]), grid_key(r))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    fetch, fmeta = load_counters(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write, wmeta = load_counters(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
+    hit, hmeta = load_counters(os.path.join(d, "l2_counter_collection.csv"), "TCC_HIT_sum")
+    miss, _ = load_counters(os.path.join(d, "l2_counter_collection.csv"), "TCC_MISS_sum")
+
+    def per_key(vals, meta):
+        acc = collections.defaultdict(list)
+        for disp, v in vals.items():
+            acc[meta[disp]].append(v)
+        return acc
+
+    F, Wr, Hh, M = per_key(fetch, fmeta), per_key(write, wmeta), per_key(hit, hmeta), per_key(miss, hmeta)
+    # finest-level dispatches: the grid with the most pixels per kernel name
+    rows = []
+    names = {}
+    for (n, g), v in dur.items():
+        tot = sum(v)
+        names.setdefault(n, []).append((g, v))
+    out = {}
+    H, W = a.H, a.W
+
+    def expected_grid(n):
+        """threads of the finest-level launch (driver.hip grid2 / pair_grid / wmf)"""
+        if n.startswith("k_pcg") or n.startswith("k_sor") or n.startswith("k_norm2"):
+            gx = (W + 127) // 128
+            return gx * 64 * min((H + 3) // 4, max(1, 512 // gx)) * 4
+        if n.startswith("k_wmf"):
+            return ((W + 7) // 8) * 64 * ((H + 7) // 8)
+        gx = (W + 63) // 64
+        return gx * 64 * min((H + 3) // 4, max(1, 2048 // gx)) * 4
+
+    for n, lst in names.items():
+        tot_ms = sum(sum(v) for _, v in lst) / 1e6
+        eg = expected_grid(n)
+        cand = [gv for gv in lst if gv[0] == eg or gv[0] == eg * 2 or gv[0] == eg * 3]
+        g, v = max(cand, key=lambda gv: len(gv[1])) if cand else max(lst, key=lambda gv: gv[0])
+        vs = sorted(v)
+        # active (non early-exit) dispatches: the upper half of durations
+        act = [x for x in vs if x >= 0.5 * vs[-1]]
+        mean_us = sum(act) / len(act) / 1e3
+        rec = {"total_ms": round(tot_ms, 3), "finest_grid": g, "finest_calls": len(v), "finest_mean_us": round(mean_us, 2)}
+        fk = [x for x in F.get((n, g), []) if x > 0]
+        wk = [x for x in Wr.get((n, g), []) if x > 0]
+        if fk:
+            fk = sorted(fk)[len(fk) // 2:]  # active dispatches
+            rec["fetch_MB"] = round(sum(fk) / len(fk) * 1024 / 1e6, 3)
+        if wk:
+            wk = sorted(wk)[len(wk) // 2:]
+            rec["write_MB"] = round(sum(wk) / len(wk) * 1024 / 1e6, 3)
+        hk, mk = Hh.get((n, g), []), M.get((n, g), [])
+        if hk and mk and sum(hk) + sum(mk) > 0:
+            rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
+        key = {"k_pcg_iter<true>": "pcg_iter", "k_pcg_iter<false>": "pcg_iter",
+               "k_flow_operator": "flow_operator", "k_wmf<3>": "wmf", "k_rof_iter": "rof_iter",
+               "k_update_occ": "update_occ", "k_partial_deriv<1>": "partial_deriv_hermite"}.get(n)
+        if key in bench.KERNEL_BYTES_PER_PX:
+            px = a.H * a.W * (2 if key == "rof_iter" else 1)
+            alg = bench.KERNEL_BYTES_PER_PX[key] * px
+            rec["alg_MB"] = round(alg / 1e6, 3)
+            rec["alg_GBps"] = round(alg / (mean_us * 1e-6) / 1e9, 1)
+            if "fetch_MB" in rec and "write_MB" in rec:
+                rec["hbm_bytes_per_launch"] = int((rec["fetch_MB"] + rec["write_MB"]) * 1e6)
+            rec["bench_name"] = key
+        out[n] = rec
+    out = dict(sorted(out.items(), key=lambda kv: -kv[1]["total_ms"]))
+    json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+    for n, r in list(out.items())[:14]:
+        print(f"{n[:34]:34s} {json.dumps(r)}")
+    if a.traffic:
+        traffic = {r["bench_name"]: {"hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"), "fetch_MB": r.get("fetch_MB"),
+                                     "write_MB": r.get("write_MB"), "grid": r["finest_grid"],
+                                     "note": "FETCH_SIZE+WRITE_SIZE (KB->B) per dispatch at the finest level; "
+                                             "FETCH_SIZE uncalibrated for <16-B/lane reads (MI355X_MICROARCH.md)"}
+                   for r in out.values() if "bench_name" in r}
+        p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+        json.dump(traffic, open(p, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
