@@ -133,17 +133,52 @@ def cpu_baseline(args):
                       f"synth_pair({args.height},{args.width},0): {dt:.2f} s, scaled x{scale:.1f} by pixel count"}
 
 
-def load_pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/pmc_traffic.json, written by profiles/collect.sh)."""
+def load_pmc_traffic(kernel, which="finest"):
+    """HBM bytes per launch of `kernel` (2*FETCH_SIZE + WRITE_SIZE) from the
+    committed rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
+    tools/prof_summary.py --traffic): averaged over all launches ("all") or
+    over the finest level's launches ("finest")."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        rec = d.get(kernel, {})
+        return rec.get("hbm_bytes_per_launch_all" if which == "all" else "hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def roofline_of(ktimes, per_level):
+    """Roofline of the dominant HBM kernel.  Top level: every launch of the
+    kernel in the timed steps (algorithmic bytes = bytes/px x the launch's
+    level pixels; duration = HIP events on the ctx stream), which is what
+    the rocprofv3 --stats average of the same kernel measures.  `finest`:
+    the same restricted to the largest level's launches."""
+    hbm = {k: v for k, v in ktimes.items() if k in KERNEL_BYTES_PER_PX}
+    if not hbm:
+        return None
+    dom = max(hbm, key=lambda k: hbm[k]["ms_total"])
+
+    def fig(rec):
+        px_per_launch = rec["px"] / rec["launches"]
+        avg_ms = rec["ms_total"] / rec["launches"]
+        ach = KERNEL_BYTES_PER_PX[dom] * px_per_launch / (avg_ms * 1e-3) / 1e9
+        return round(ach, 1), round(avg_ms, 5), int(px_per_launch)
+
+    ach, avg_ms, ppl = fig(hbm[dom])
+    out = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, "all"),
+           "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": avg_ms, "px_per_launch": ppl,
+           "launches_per_step": hbm[dom]["launches"]}
+    lv = [(px, rec) for (n, px), rec in per_level.items() if n == dom]
+    if lv:
+        px, rec = max(lv, key=lambda t: t[0])
+        a2, m2, p2 = fig(rec)
+        out["finest"] = {"px_per_launch": p2, "achieved": a2, "frac": round(a2 / HBM_PEAK_GBS, 4),
+                         "mean_launch_ms": m2, "launches_per_step": rec["launches"],
+                         "traffic": load_pmc_traffic(dom, "finest")}
+    return out
 
 
 def main():
@@ -203,34 +238,25 @@ def main():
     if not args.no_profile:
         # profiled replay of the timed steps: HIP events around every launch
         # on the ctx stream (the stream the kernels run on)
-        ctx.check(lib.of_set_profiling(ctx.handle, 1))
+        ctx.check(lib.of_set_profiling(ctx.handle, 2))  # keyed by kernel and level size
         for _ in range(args.steps):
             run_step(ctx, P0, args.pairs)
         n = C.c_int(0)
-        names = (C.c_char_p * 256)()
-        ms = (C.c_double * 256)()
-        cnt = (C.c_int64 * 256)()
-        pxs = (C.c_double * 256)()
-        ctx.check(lib.of_kernel_times(ctx.handle, 256, names, ms, cnt, pxs, C.byref(n)))
+        names = (C.c_char_p * 1024)()
+        ms = (C.c_double * 1024)()
+        cnt = (C.c_int64 * 1024)()
+        pxs = (C.c_double * 1024)()
+        ctx.check(lib.of_kernel_times(ctx.handle, 1024, names, ms, cnt, pxs, C.byref(n)))
         ctx.check(lib.of_set_profiling(ctx.handle, 0))
-        for i in range(n.value):
-            ktimes[names[i].decode()] = {"ms_total": ms[i] / args.steps, "launches": int(cnt[i]) / args.steps,
-                                         "px": pxs[i] / args.steps}
-        hbm = {k: v for k, v in ktimes.items() if k in KERNEL_BYTES_PER_PX}
-        if hbm:
-            dom = max(hbm, key=lambda k: hbm[k]["ms_total"])
-            # algorithmic bytes per launch = bytes/px x pixels of the level the
-            # launch ran on (exact per-launch pixel counts from the library)
-            px_per_launch = hbm[dom]["px"] / hbm[dom]["launches"]
-            avg_ms = hbm[dom]["ms_total"] / hbm[dom]["launches"]
-            bytes_per_launch = KERNEL_BYTES_PER_PX[dom] * px_per_launch
-            ach = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": load_pmc_traffic(dom),
-                        "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": round(avg_ms, 5),
-                        "px_per_launch": int(px_per_launch)}
-
+        per_level = {}
+        for i in range(min(n.value, 1024)):
+            name, lvl = names[i].decode().rsplit("@", 1)
+            rec = {"ms_total": ms[i] / args.steps, "launches": int(cnt[i]) / args.steps, "px": pxs[i] / args.steps}
+            per_level[(name, int(lvl))] = rec
+            agg = ktimes.setdefault(name, {"ms_total": 0.0, "launches": 0.0, "px": 0.0})
+            for k in agg:
+                agg[k] += rec[k]
+        roofline = roofline_of(ktimes, per_level)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)

@@ -141,7 +141,9 @@ int of_ctx_create(int device, of_ctx **out);
 int of_ctx_destroy(of_ctx *ctx);
 const char *of_last_error(of_ctx *ctx);
 int of_synchronize(of_ctx *ctx);
-/* per-kernel HIP-event timing on the ctx stream (0 = off); see of_kernel_times */
+/* per-kernel HIP-event timing on the ctx stream: 0 = off, 1 = keyed by kernel
+ * name, 2 = keyed by "name@pixels" (one entry per kernel and level size);
+ * see of_kernel_times */
 int of_set_profiling(of_ctx *ctx, int enable);
 /* kernel timing accumulated since enable: per kernel name total ms, launch
  * count and pixels processed (sum over launches of the level's H*W; ROF

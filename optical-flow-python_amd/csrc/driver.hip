@@ -111,7 +111,7 @@ struct of_ctx {
   unsigned *d_counter = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
-  bool prof = false;
+  int prof = 0;  // 0 off, 1 per kernel, 2 per kernel and level ("name@pixels")
   std::vector<hipEvent_t> ev_pool;  // profiling events
   size_t ev_used = 0;
   std::vector<hipEvent_t> tev_pool;  // level timing events, recycled per API call
@@ -152,7 +152,8 @@ void flush_prof(of_ctx *c) {
   for (auto &r : c->pending) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
-    auto &s = c->ktimes[r.name];
+    auto &s = c->prof == 2 ? c->ktimes[std::string(r.name) + "@" + std::to_string((long long)r.px)]
+                           : c->ktimes[r.name];
     s.ms += ms;
     s.px += r.px;
     s.n += 1;
@@ -1012,7 +1013,7 @@ int of_set_profiling(of_ctx *c, int enable) {
   } catch (const OfError &e) {
     return fail(c, e);
   }
-  c->prof = enable != 0;
+  c->prof = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
   if (enable) c->ktimes.clear();
   return OF_OK;
 }

@@ -1,0 +1,94 @@
+"""Multi-GPU bench path on CPU: world size 2 over gloo.
+
+bench.py shards pairs one process per GPU (pair k of the global batch on
+rank k // P), times each rank between barriers and reports the max over
+ranks; gloo carries only the barrier, the max-reduce and the RCCL unique-id
+broadcast.  These tests run exactly those functions in two CPU processes.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, pairs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    dist, w, r, local = bench.dist_setup(None)
+    assert (w, r, local) == (world, rank, rank)
+    seeds = bench.shard_seeds(r, pairs)
+    # every rank's seeds, gathered on every rank (test-side only)
+    allseeds = [None] * w
+    dist.all_gather_object(allseeds, seeds)
+    bench.barrier(dist)
+    t = bench.max_over_ranks(dist, 1.0 + rank)  # rank r "took" 1+r seconds
+    # RCCL unique-id broadcast as bench.main does it (bytes object from rank 0)
+    obj = [bytes([7] * 128) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    q.put((rank, seeds, allseeds, t, obj[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pairs", [1, 3])
+def test_bench_sharding_world2(pairs):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pairs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    flat = sorted(s for _, _, allseeds, _, _ in res[:1] for ss in allseeds for s in ss)
+    # the global batch is covered exactly once: seeds 0 .. world*pairs-1
+    assert flat == list(range(world * pairs))
+    for rank, seeds, allseeds, t, uid in res:
+        assert seeds == list(range(rank * pairs, (rank + 1) * pairs))
+        assert allseeds == res[0][2]
+        assert t == pytest.approx(float(world))  # max over ranks
+        assert uid == bytes([7] * 128)
+
+
+def test_bench_single_process_defaults(monkeypatch):
+    import bench
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    dist, w, r, local = bench.dist_setup(None)
+    assert dist is None and (w, r, local) == (1, 0, 0)
+    assert bench.max_over_ranks(None, 3.5) == 3.5
+    assert bench.shard_seeds(0, 2) == [0, 1]
+
+
+def test_roofline_of_all_and_finest():
+    import bench
+    per_level = {("pcg_iter", 1000): {"ms_total": 2.0, "launches": 10, "px": 1e10},
+                 ("pcg_iter", 100): {"ms_total": 1.0, "launches": 10, "px": 1e9},
+                 ("wmf", 1000): {"ms_total": 0.5, "launches": 1, "px": 1000.0}}
+    kt = {}
+    for (n, _), rec in per_level.items():
+        a = kt.setdefault(n, {"ms_total": 0.0, "launches": 0.0, "px": 0.0})
+        for k in a:
+            a[k] += rec[k]
+    r = bench.roofline_of(kt, per_level)
+    bpp = bench.KERNEL_BYTES_PER_PX["pcg_iter"]
+    assert r["kernel"] == "pcg_iter"
+    assert r["achieved"] == pytest.approx(bpp * 5.5e8 / 0.15e-3 / 1e9, rel=1e-3)
+    assert r["finest"]["achieved"] == pytest.approx(bpp * 1e9 / 0.2e-3 / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)

@@ -1,0 +1,77 @@
+"""Device-resident batch path (bench.py / config 5): of_pair_upload/run/
+download and the RCCL gather, on one GPU.
+
+A world-size-1 RCCL communicator exercises of_rccl_init and the gather's
+send/recv group; the multi-rank sharding logic around it is covered on CPU by
+tests/test_dist_cpu.py (gloo, world size 2)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(method):
+    from optical_flow.methods.config import load_of_method
+    ope = load_of_method(method)
+    P = ope.to_params()
+    P.guide_mode = int(ope._METHOD == "classic_nl" and ope.color_images is not None)
+    P.display = 0
+    return P
+
+
+def _run_slots(ctx, P0, n):
+    from optical_flow import _abi
+    for s in range(n):
+        P = _abi.OfParams()
+        C.memmove(C.byref(P), C.byref(P0), C.sizeof(P0))
+        ctx.check(ctx.lib.of_pair_run(ctx.handle, s, C.byref(P), None))
+
+
+def test_pair_slots_match_estimate_flow():
+    """A slot run equals estimate_flow on the same pair (same kernels)."""
+    import optical_flow
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    H, W = 60, 88
+    pairs = [synth_pair(H, W, k) for k in range(3)]
+    for s, (a, b, _) in enumerate(pairs):
+        ctx.check(ctx.lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
+                                         H, W, 3))
+    _run_slots(ctx, _params("classic+nl-fast"), 3)
+    for s, (a, b, _) in enumerate(pairs):
+        uv = np.empty((2, H, W), np.float32)
+        ctx.check(ctx.lib.of_pair_download(ctx.handle, s, _native.ptr(uv)))
+        ref = optical_flow.estimate_flow(a, b, "classic+nl-fast")
+        np.testing.assert_allclose(np.moveaxis(uv, 0, 2), ref, atol=1e-5)
+    ctx.close()
+
+
+def test_rccl_gather_single_rank():
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    lib = ctx.lib
+    H, W = 40, 56
+    for s in range(2):
+        a, b, _ = synth_pair(H, W, 10 + s)
+        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
+                                     H, W, 3))
+    _run_slots(ctx, _params("hs"), 2)
+    uid = C.create_string_buffer(128)
+    ctx.check(lib.of_rccl_unique_id(uid))
+    ctx.check(lib.of_rccl_init(ctx.handle, uid.raw, 1, 0))
+    try:
+        out = np.full((2, 2, H, W), np.nan, np.float32)
+        ctx.check(lib.of_rccl_gather_flows(ctx.handle, 2, _native.ptr(out)))
+        for s in range(2):
+            uv = np.empty((2, H, W), np.float32)
+            ctx.check(lib.of_pair_download(ctx.handle, s, _native.ptr(uv)))
+            np.testing.assert_array_equal(out[s], uv)
+        with pytest.raises(ValueError):
+            ctx.check(lib.of_rccl_gather_flows(ctx.handle, 5, None))  # more slots than uploaded
+    finally:
+        lib.of_rccl_finalize(ctx.handle)
+        ctx.close()

@@ -116,18 +116,31 @@ def main():
             rec["alg_MB"] = round(alg / 1e6, 3)
             rec["alg_GBps"] = round(alg / (mean_us * 1e-6) / 1e9, 1)
             if "fetch_MB" in rec and "write_MB" in rec:
-                rec["hbm_bytes_per_launch"] = int((rec["fetch_MB"] + rec["write_MB"]) * 1e6)
+                # FETCH_SIZE counts 64 B per 128-B request on gfx950
+                # (MI355X_MICROARCH.md HBM section; re-checked on k_rof_iter's
+                # known byte count): double it, WRITE_SIZE is exact
+                rec["hbm_bytes_per_launch"] = int((2 * rec["fetch_MB"] + rec["write_MB"]) * 1e6)
             rec["bench_name"] = key
+            # every dispatch of the kernel (all levels, incl. converged no-op
+            # CG launches): comparable with bench.py's all-launch roofline
+            fa = [v for disp, v in fetch.items() if fmeta[disp][0] == n]
+            wa = [v for disp, v in write.items() if wmeta[disp][0] == n]
+            if fa and wa:
+                rec["hbm_bytes_per_launch_all"] = int((2 * sum(fa) / len(fa) + sum(wa) / len(wa)) * 1024)
         out[n] = rec
     out = dict(sorted(out.items(), key=lambda kv: -kv[1]["total_ms"]))
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
     for n, r in list(out.items())[:14]:
         print(f"{n[:34]:34s} {json.dumps(r)}")
     if a.traffic:
-        traffic = {r["bench_name"]: {"hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"), "fetch_MB": r.get("fetch_MB"),
+        traffic = {r["bench_name"]: {"hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"),
+                                     "hbm_bytes_per_launch_all": r.get("hbm_bytes_per_launch_all"),
+                                     "fetch_MB": r.get("fetch_MB"),
                                      "write_MB": r.get("write_MB"), "grid": r["finest_grid"],
-                                     "note": "FETCH_SIZE+WRITE_SIZE (KB->B) per dispatch at the finest level; "
-                                             "FETCH_SIZE uncalibrated for <16-B/lane reads (MI355X_MICROARCH.md)"}
+                                     "l2_hit": r.get("l2_hit"),
+                                     "note": "2*FETCH_SIZE + WRITE_SIZE (KB->B) per dispatch at the finest level "
+                                             "(FETCH_SIZE x2: gfx950 tallies 128-B requests at 64 B); "
+                                             "Infinity-Cache (MALL) hits are included in FETCH_SIZE"}
                    for r in out.values() if "bench_name" in r}
         p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
         json.dump(traffic, open(p, "w"), indent=1)
