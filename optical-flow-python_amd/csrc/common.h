@@ -115,46 +115,6 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *lds /* NV*16 
     }
 }
 
-// Last-block-done hand-off (cdna_hip_programming.md §6 Guideline 16):
-// thread 0 stores the block partials, releases at agent scope and takes a
-// ticket; the block drawing nblocks-1 acquires and may read every partial.
-template <int NV>
-__device__ __forceinline__ bool arrive_last(const double (&v)[NV], double *partials, unsigned *counter, int nblocks,
-                                            int bid) {
-  __shared__ int s_last;
-  const int tid = threadIdx.x + threadIdx.y * blockDim.x;
-  if (tid == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) partials[(size_t)k * nblocks + bid] = v[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int last = prev == (unsigned)(nblocks - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  return s_last != 0;
-}
-
-// In the last block: fixed-order sum of NV partial arrays (deterministic).
-template <int NV>
-__device__ __forceinline__ void final_sum(double (&out)[NV], const double *partials, int nblocks, double *lds) {
-  const int tid = threadIdx.x + threadIdx.y * blockDim.x;
-  const int nt = blockDim.x * blockDim.y;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double s = 0;
-    for (int b = tid; b < nblocks; b += nt) s += partials[(size_t)k * nblocks + b];
-    out[k] = s;
-  }
-  __syncthreads();
-  block_sum<NV>(out, lds);
-}
-
 // ---- launch geometry: 64x4 blocks, grid-stride over row groups ----------
 struct Grid2 {
   dim3 grid, block;

@@ -108,7 +108,6 @@ struct of_ctx {
   PcgState *d_state = nullptr, *h_state = nullptr;  // h_state: 2 pinned slots
   hipEvent_t ev_state[2] = {nullptr, nullptr};
   double *d_partials = nullptr;
-  unsigned *d_counter = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
   int prof = 0;  // 0 off, 1 per kernel, 2 per kernel and level ("name@pixels")
@@ -125,8 +124,6 @@ struct of_ctx {
 };
 
 namespace {
-
-constexpr int MAX_RED_BLOCKS = 2048;
 
 hipEvent_t pool_event(of_ctx *c) {
   if (c->ev_used == c->ev_pool.size()) {
@@ -604,17 +601,21 @@ void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &
   REQUIRE(guide.C == 1 || guide.C == 3, OF_ENOTSUP, "weighted median guide must have 1 or 3 channels");
   REQUIRE(hsz >= 0 && hsz <= 12, OF_ENOTSUP, "area_hsz must be <= 12");
   const int RW = WMF_T + 2 * hsz, nreg = RW * RW;
-  int npow2 = 1;
+  int npow2 = 64;
   while (npow2 < nreg) npow2 <<= 1;
-  const size_t shm = 2 * (size_t)npow2 * sizeof(uint64_t) + (size_t)(guide.C + 1) * nreg * sizeof(float);
+  const int nper = npow2 / 64;  // sort keys per lane: 1..16
+  const size_t shm = 2 * (size_t)npow2 * sizeof(uint16_t) + (size_t)nreg * (guide.C == 3 ? 16 : 8);
   dim3 grid((uv.W + WMF_T - 1) / WMF_T, (uv.H + WMF_T - 1) / WMF_T);
-  const float inv = (float)(1.0 / (2.0 * sigma_i * sigma_i));
+  const float nk = (float)(-1.4426950408889634 / (2.0 * sigma_i * sigma_i));  // -log2(e) / (2 sigma^2)
+  auto pick = [&](auto k1, auto k2, auto k4, auto k8, auto k16) {
+    auto k = nper == 1 ? k1 : nper == 2 ? k2 : nper == 4 ? k4 : nper == 8 ? k8 : k16;
+    launch(c, "wmf", k, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H, uv.W,
+           uv.P, guide.ps(), hsz, nk, RW, nreg);
+  };
   if (guide.C == 3)
-    launch(c, "wmf", k_wmf<3>, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H,
-           uv.W, uv.P, guide.ps(), hsz, inv, RW, nreg, npow2);
+    pick(k_wmf<3, 1>, k_wmf<3, 2>, k_wmf<3, 4>, k_wmf<3, 8>, k_wmf<3, 16>);
   else
-    launch(c, "wmf", k_wmf<1>, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H,
-           uv.W, uv.P, guide.ps(), hsz, inv, RW, nreg, npow2);
+    pick(k_wmf<1, 1>, k_wmf<1, 2>, k_wmf<1, 4>, k_wmf<1, 8>, k_wmf<1, 16>);
 }
 
 void resample_f2(of_ctx *c, const F2 &in, const F2 &out) {
@@ -958,8 +959,6 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
     HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 8 * PCG_MAX_BLOCKS));
-    HIPCHK(hipMalloc(&c->d_counter, sizeof(unsigned) * 16));
-    HIPCHK(hipMemset(c->d_counter, 0, sizeof(unsigned) * 16));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
     HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));
@@ -990,7 +989,6 @@ int of_ctx_destroy(of_ctx *c) {
   hipFree(c->d_state);
   hipHostFree(c->h_state);
   hipFree(c->d_partials);
-  hipFree(c->d_counter);
   hipFree(c->d_mm);
   hipFree(c->d_norm);
   hipHostFree(c->h_norm);

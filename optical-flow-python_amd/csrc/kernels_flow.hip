@@ -366,97 +366,196 @@ __global__ void k_lo_blend(const float2 *__restrict__ u, const float2 *__restric
 
 // ---------------------------------------------------------------------------
 // Occlusion-weighted, colour-guided weighted median
-// (weighted_median.py:24-112).  One wave per 8x8 output tile:
-//  1. stage the (8+2h)^2 region (whole-sample mirror padding = np.pad
-//     'reflect') in LDS: u, v sort keys, guide channels, occlusion;
-//  2. bitonic-sort the u keys and the v keys once per tile;
-//  3. every lane (output pixel) sums its window weights, then walks the
-//     sorted region list in lockstep with the other lanes (broadcast LDS
-//     reads), accumulating only samples inside its own window, and stops at
-//     the first sample whose cumulative weight reaches half the total:
-//     exactly np.searchsorted(cumsum(w_sorted), total / 2).
+// (denoise_color_weighted_medfilt2, weighted_median.py:24-112).  One wave per 8x8 tile:
+//  1. the (8+2h)^2 region is loaded straight into registers, NPER keys per
+//     lane (element e = lane*NPER + r), and guide+occ records go to LDS;
+//  2. u and v keys are bitonic-sorted in registers: stages with partner
+//     distance < NPER swap registers, the others exchange with lane^(d/NPER)
+//     by ds_bpermute (no LDS storage, no barriers);
+//  3. sorted keys go to LDS; every lane walks both lists in lockstep, 8 keys
+//     per batch, weights of the u and v samples computed in packed fp32
+//     (v_pk_*), fp64 cumulative sums advanced branch-free in sorted order.
+// Weight = max(2^(-|dlab|^2 * log2e/(2 sigma^2)) * occ, 1e-10) (v_exp_f32);
+// result = the first sorted value with cumsum >= total/2
+// (weighted_median.py:5-21, :67-112).
 #define WMF_T 8
 template <int GC>
+struct WmfRec;
+template <>
+struct WmfRec<3> {
+  using T = float4;
+  __device__ static T make(float a, float b, float c, float o) { return make_float4(a, b, c, o); }
+  __device__ static float d2(const T &s, const float *cg) {
+    const float e0 = s.x - cg[0], e1 = s.y - cg[1], e2 = s.z - cg[2];
+    return e0 * e0 + e1 * e1 + e2 * e2;
+  }
+  __device__ static float occ(const T &s) { return s.w; }
+};
+template <>
+struct WmfRec<1> {
+  using T = float2;
+  __device__ static T make(float a, float, float, float o) { return make_float2(a, o); }
+  __device__ static float d2(const T &s, const float *cg) {
+    const float e0 = s.x - cg[0];
+    return e0 * e0;
+  }
+  __device__ static float occ(const T &s) { return s.y; }
+};
+
+typedef float wmf_v2f __attribute__((ext_vector_type(2)));
+
+template <int NPER>
+__device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
+  constexpr int N = NPER * 64;
+#pragma unroll
+  for (int kk = 2; kk <= N; kk <<= 1) {
+#pragma unroll
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      if (jj >= NPER) {
+        const int lj = jj / NPER;
+        const bool lower = (lane & lj) == 0;
+#pragma unroll
+        for (int r = 0; r < NPER; ++r) {
+          const bool up = (((lane * NPER + r) & kk) == 0);
+          const uint64_t o = __shfl_xor(k[r], lj);
+          const bool take_min = lower == up;
+          const uint64_t mn = k[r] < o ? k[r] : o, mx = k[r] < o ? o : k[r];
+          k[r] = take_min ? mn : mx;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < NPER; ++r) {
+          const int rp = r ^ jj;
+          if (rp > r) {
+            const bool up = (((lane * NPER + r) & kk) == 0);
+            const uint64_t a = k[r], b = k[rp];
+            const bool sw = (a > b) == up;
+            k[r] = sw ? b : a;
+            k[rp] = sw ? a : b;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int GC, int NPER>
 __global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
-                                            const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
-                                            int P, size_t ps, int hsz, float inv2s2, int RW, int nreg, int npow2) {
+                                             const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
+                                             int P, size_t ps, int hsz, float nk, int RW, int nreg) {
+  using R = WmfRec<GC>;
+  using T = typename R::T;
+  constexpr int N = NPER * 64;
+  // LDS: sorted region positions (ry << 8 | rx) of the u and v lists, then
+  // the guide+occ records: 2*N*2 + nreg*sizeof(T) bytes (9.8 KB at h = 7)
   extern __shared__ uint64_t lds_u64[];
-  uint64_t *ku = lds_u64, *kv = lds_u64 + npow2;
-  float *smp = reinterpret_cast<float *>(lds_u64 + 2 * npow2);  // [GC+1][nreg]
+  T *smp = reinterpret_cast<T *>(lds_u64);  // [nreg]
+  uint16_t *ku = reinterpret_cast<uint16_t *>(smp + nreg), *kv = ku + N;
   const int ty0 = blockIdx.y * WMF_T, tx0 = blockIdx.x * WMF_T;
-  const int t = threadIdx.x;
-  for (int s = t; s < npow2; s += 64) {
+  const int lane = threadIdx.x;
+  uint64_t a[NPER], b[NPER];
+#pragma unroll
+  for (int r = 0; r < NPER; ++r) {
+    const int s = lane * NPER + r;
+    a[r] = ~0ull;
+    b[r] = ~0ull;
     if (s < nreg) {
       const int ry = s / RW, rx = s - ry * RW;
       const size_t g = (size_t)ext_mirror(ty0 - hsz + ry, H) * P + ext_mirror(tx0 - hsz + rx, W);
       const float2 v = uv[g];
-      const uint64_t lo = ((uint64_t)ry << 16) | (uint64_t)rx;
-      ku[s] = ((uint64_t)f2ord(v.x) << 32) | lo;
-      kv[s] = ((uint64_t)f2ord(v.y) << 32) | lo;
+      const uint64_t lo = ((uint64_t)ry << 8) | (uint64_t)rx;
+      a[r] = ((uint64_t)f2ord(v.x) << 32) | lo;
+      b[r] = ((uint64_t)f2ord(v.y) << 32) | lo;
+      float gv[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < GC; ++c) smp[c * nreg + s] = guide[c * ps + g];
-      smp[GC * nreg + s] = occ[g];
-    } else {
-      ku[s] = ~0ull;
-      kv[s] = ~0ull;
+      for (int c = 0; c < GC; ++c) gv[c] = guide[c * ps + g];
+      smp[s] = R::make(gv[0], gv[1], gv[2], occ[g]);
     }
+  }
+  bitonic_regs<NPER>(a, lane);
+  bitonic_regs<NPER>(b, lane);
+#pragma unroll
+  for (int r = 0; r < NPER; ++r) {
+    ku[lane * NPER + r] = (uint16_t)a[r];  // padding keys -> 0xffff: out of every window
+    kv[lane * NPER + r] = (uint16_t)b[r];
   }
   __syncthreads();
-  for (int kk = 2; kk <= npow2; kk <<= 1)
-    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (int idx = t; idx < npow2; idx += 64) {
-        const int ixj = idx ^ jj;
-        if (ixj > idx) {
-          const bool up = (idx & kk) == 0;
-          uint64_t a = ku[idx], b = ku[ixj];
-          if ((a > b) == up) { ku[idx] = b; ku[ixj] = a; }
-          a = kv[idx];
-          b = kv[ixj];
-          if ((a > b) == up) { kv[idx] = b; kv[ixj] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  const int py = t >> 3, px = t & 7;
+  const int py = lane >> 3, px = lane & 7;
   const int gi = ty0 + py, gj = tx0 + px;
-  if (gi >= H || gj >= W) return;
-  const int cy = py + hsz, cx = px + hsz;
-  float cg[GC];
+  const bool live = gi < H && gj < W;  // dead lanes still walk (wave-uniform exit)
+  float cg[3] = {0.f, 0.f, 0.f};
+  {
+    const T c0 = smp[(py + hsz) * RW + px + hsz];
+    const float *cf = reinterpret_cast<const float *>(&c0);
 #pragma unroll
-  for (int c = 0; c < GC; ++c) cg[c] = smp[c * nreg + cy * RW + cx];
-  auto weight = [&](int s) {
-    float d2 = 0.0f;
-#pragma unroll
-    for (int c = 0; c < GC; ++c) {
-      const float e = smp[c * nreg + s] - cg[c];
-      d2 += e * e;
-    }
-    return fmaxf(expf(-d2 * inv2s2) * smp[GC * nreg + s], 1e-10f);
-  };
-  double tot = 0.0;
-  for (int dy = -hsz; dy <= hsz; ++dy)
-    for (int dx = -hsz; dx <= hsz; ++dx) tot += (double)weight((cy + dy) * RW + cx + dx);
-  const double half = 0.5 * tot;
-  float res[2] = {0.0f, 0.0f};
-#pragma unroll
-  for (int comp = 0; comp < 2; ++comp) {
-    const uint64_t *keys = comp ? kv : ku;
-    double cum = 0.0;
-    float last = 0.0f;
-    for (int k = 0; k < nreg; ++k) {
-      const uint64_t key = keys[k];
-      const int ry = (int)((key >> 16) & 0xffff), rx = (int)(key & 0xffff);
-      if (abs(ry - cy) <= hsz && abs(rx - cx) <= hsz) {
-        last = ord2f((uint32_t)(key >> 32));
-        cum += (double)weight(ry * RW + rx);
-        if (cum >= half) break;
-      }
-    }
-    res[comp] = last;
+    for (int c = 0; c < GC; ++c) cg[c] = cf[c];
   }
-  out[(size_t)gi * P + gj] = make_float2(res[0], res[1]);
+  // total weight of the lane's window (row-major window order)
+  double tot = 0.0;
+  for (int dy = 0; dy <= 2 * hsz; ++dy) {
+    const T *row = smp + (py + dy) * RW + px;
+    for (int dx = 0; dx <= 2 * hsz; ++dx) {
+      const T s = row[dx];
+      tot += (double)fmaxf(__builtin_amdgcn_exp2f(R::d2(s, cg) * nk) * R::occ(s), 1e-10f);
+    }
+  }
+  const double half = 0.5 * tot;
+  const unsigned span = 2u * hsz;
+  double cu = 0.0, cv = 0.0;
+  unsigned resu = 0, resv = 0;
+  bool du = !live, dv = !live;
+  for (int k0 = 0; k0 < N; k0 += 8) {
+    unsigned ka[8], kb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ka[i] = ku[k0 + i];
+      kb[i] = kv[k0 + i];
+    }
+    wmf_v2f w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu, ryb = kb[i] >> 8, rxb = kb[i] & 0xffu;
+      const bool ina = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
+      const bool inb = (ryb - (unsigned)py) <= span && (rxb - (unsigned)px) <= span;
+      const T sa = smp[ina ? rya * RW + rxa : 0];
+      const T sb = smp[inb ? ryb * RW + rxb : 0];
+      const float *fa = reinterpret_cast<const float *>(&sa);
+      const float *fb = reinterpret_cast<const float *>(&sb);
+      wmf_v2f d2 = {0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < GC; ++c) {
+        const wmf_v2f e = wmf_v2f{fa[c], fb[c]} - cg[c];
+        d2 += e * e;
+      }
+      d2 *= nk;
+      wmf_v2f ww = {__builtin_amdgcn_exp2f(d2.x), __builtin_amdgcn_exp2f(d2.y)};
+      ww *= wmf_v2f{R::occ(sa), R::occ(sb)};
+      ww.x = ina ? fmaxf(ww.x, 1e-10f) : 0.0f;
+      ww.y = inb ? fmaxf(ww.y, 1e-10f) : 0.0f;
+      w[i] = ww;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      cu += (double)w[i].x;
+      cv += (double)w[i].y;
+      const bool xa = !du && cu >= half, xb = !dv && cv >= half;
+      resu = xa ? ka[i] : resu;
+      resv = xb ? kb[i] : resv;
+      du = du || xa;
+      dv = dv || xb;
+    }
+    if (__all(du && dv)) break;
+  }
+  if (live) {
+    // the selected samples' values, re-read at their (mirrored) positions
+    const int ya = ext_mirror(ty0 - hsz + (int)(resu >> 8), H), xa = ext_mirror(tx0 - hsz + (int)(resu & 0xffu), W);
+    const int yb = ext_mirror(ty0 - hsz + (int)(resv >> 8), H), xb = ext_mirror(tx0 - hsz + (int)(resv & 0xffu), W);
+    out[(size_t)gi * P + gj] = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
+  }
 }
-template __global__ void k_wmf<1>(const float2 *, const float *, const float *, float2 *, int, int, int, size_t, int,
-                                  float, int, int, int);
-template __global__ void k_wmf<3>(const float2 *, const float *, const float *, float2 *, int, int, int, size_t, int,
-                                  float, int, int, int);
+#define OF_WMF(GC, NP)                                                                                           \
+  template __global__ void k_wmf<GC, NP>(const float2 *, const float *, const float *, float2 *, int, int, int, \
+                                          size_t, int, float, int, int);
+OF_WMF(1, 1) OF_WMF(1, 2) OF_WMF(1, 4) OF_WMF(1, 8) OF_WMF(1, 16)
+OF_WMF(3, 1) OF_WMF(3, 2) OF_WMF(3, 4) OF_WMF(3, 8) OF_WMF(3, 16)
+#undef OF_WMF

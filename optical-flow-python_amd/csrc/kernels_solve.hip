@@ -101,157 +101,6 @@ struct PcgArgs {
   int maxiter;
 };
 
-// x = 0, r = b, z = M^-1 b; partials r.z, r.r
-template <bool BLOCK>
-__global__ __launch_bounds__(256) void k_pcg_init(PcgArgs a) {
-  __shared__ double lds[32];
-  double v[2] = {0.0, 0.0};
-  const float *A = a.coef + 4 * a.ps, *Cc = a.coef + 5 * a.ps, *D = a.coef + 6 * a.ps;
-  OF_FOR_PIXEL_PAIRS(a.H, a.W) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = j0 + e;
-      if (j >= a.W) break;
-      const size_t k = (size_t)i * a.P + j;
-      const float2 bb = a.b[k];
-      const float2 zz = precond<BLOCK>(A[k], Cc[k], D[k], bb);
-      a.x[k] = make_float2(0.0f, 0.0f);
-      a.r[k] = bb;
-      a.z[k] = zz;
-      v[0] += (double)bb.x * zz.x + (double)bb.y * zz.y;
-      v[1] += (double)bb.x * bb.x + (double)bb.y * bb.y;
-    }
-  }
-  write_partials<2>(v, a.part + PCG_MAX_BLOCKS, lds);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
-    a.st->done = a.maxiter <= 0 ? 2 : 0;
-    a.st->iter = 0;
-    a.st->maxiter = a.maxiter;
-  }
-}
-
-__device__ __forceinline__ float2 lin(float2 z, float2 p, float beta) {
-  return make_float2(z.x + beta * p.x, z.y + beta * p.y);
-}
-
-// p_new = z + beta p_old (p = z when k == 0), q = A p_new; partial p.q
-__global__ __launch_bounds__(256) void k_pcg_dir_spmv(PcgArgs a, int k) {
-  __shared__ double lds[32];
-  __shared__ int s_exit;
-  if (a.st->done) return;
-  double sums[2];
-  prologue_sum<2>(sums, a.part + PCG_MAX_BLOCKS, a.nb, lds);  // r.z, r.r of update(k-1) / init
-  const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0;
-  double beta_d = 0.0;
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
-    int done = 0;
-    double atol;
-    if (k == 0) {
-      const double bn = sqrt(sums[1]);
-      atol = a.rtol * bn;
-      if (lead) { a.st->bnorm = bn; a.st->atol = atol; }
-      if (bn == 0.0) done = 3;
-    } else {
-      atol = a.st->atol;
-      beta_d = sums[0] / a.st->rho[(k - 1) & 1];
-    }
-    if (!done && sqrt(sums[1]) < atol) done = 1;  // scipy cg: check before the iteration
-    if (!done && k >= a.maxiter) done = 2;
-    if (lead) {
-      a.st->rho[k & 1] = sums[0];
-      a.st->rr = sums[1];
-      a.st->iter = k;
-      if (done) a.st->done = done;
-    }
-    s_exit = done;
-    lds[31] = beta_d;
-  }
-  __syncthreads();
-  if (s_exit) return;
-  const float beta = (float)lds[31];
-  const bool first = k == 0;
-  const float *wxu = a.coef, *wyu = a.coef + a.ps, *wxv = a.coef + 2 * a.ps, *wyv = a.coef + 3 * a.ps;
-  const float *A = a.coef + 4 * a.ps, *Cc = a.coef + 5 * a.ps, *D = a.coef + 6 * a.ps;
-  const int H = a.H, W = a.W, P = a.P;
-  double v[1] = {0.0};
-  OF_FOR_PIXEL_PAIRS(H, W) {
-    if (j0 >= W) continue;
-    const size_t k0 = (size_t)i * P + j0;
-    const bool two = j0 + 1 < W;
-    // p at this pair and its 4-neighbourhood
-    auto pn = [&](size_t kk) -> float2 { return first ? a.z[kk] : lin(a.z[kk], a.p_old[kk], beta); };
-    const float2 c0 = pn(k0), c1 = two ? pn(k0 + 1) : make_float2(0.f, 0.f);
-    const float2 l0 = j0 > 0 ? pn(k0 - 1) : make_float2(0.f, 0.f);
-    const float2 r1 = j0 + 2 < W ? pn(k0 + 2) : make_float2(0.f, 0.f);
-    a.p_new[k0] = c0;
-    if (two) a.p_new[k0 + 1] = c1;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      if (e == 1 && !two) break;
-      const int j = j0 + e;
-      const size_t kk = k0 + e;
-      const float2 c = e ? c1 : c0;
-      const float2 L = e ? c0 : l0, R = e ? r1 : c1;
-      float su = 0.0f, sv = 0.0f;
-      if (j < W - 1) { su += wxu[kk] * R.x; sv += wxv[kk] * R.y; }
-      if (j > 0) { su += wxu[kk - 1] * L.x; sv += wxv[kk - 1] * L.y; }
-      if (i < H - 1) { const float2 n = pn(kk + P); su += wyu[kk] * n.x; sv += wyv[kk] * n.y; }
-      if (i > 0) { const float2 n = pn(kk - P); su += wyu[kk - P] * n.x; sv += wyv[kk - P] * n.y; }
-      const float aa = A[kk], cc = Cc[kk], dd = D[kk];
-      const float2 qq = make_float2(aa * c.x + cc * c.y - su, cc * c.x + dd * c.y - sv);
-      a.q[kk] = qq;
-      v[0] += (double)c.x * qq.x + (double)c.y * qq.y;
-    }
-  }
-  write_partials<1>(v, a.part, lds);
-}
-
-// x += alpha p, r -= alpha q, z = M^-1 r; partials r.z, r.r
-template <bool BLOCK>
-__global__ __launch_bounds__(256) void k_pcg_update(PcgArgs a, int k) {
-  __shared__ double lds[32];
-  if (a.st->done) return;
-  double pq[1];
-  prologue_sum<1>(pq, a.part, a.nb, lds);
-  const float alpha = (float)(a.st->rho[k & 1] / pq[0]);
-  const float *A = a.coef + 4 * a.ps, *Cc = a.coef + 5 * a.ps, *D = a.coef + 6 * a.ps;
-  double v[2] = {0.0, 0.0};
-  OF_FOR_PIXEL_PAIRS(a.H, a.W) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = j0 + e;
-      if (j >= a.W) break;
-      const size_t kk = (size_t)i * a.P + j;
-      const float2 pp = a.p_new[kk], qq = a.q[kk];
-      float2 xx = a.x[kk], rr = a.r[kk];
-      xx.x += alpha * pp.x;
-      xx.y += alpha * pp.y;
-      rr.x -= alpha * qq.x;
-      rr.y -= alpha * qq.y;
-      a.x[kk] = xx;
-      a.r[kk] = rr;
-      const float2 zz = precond<BLOCK>(A[kk], Cc[kk], D[kk], rr);
-      a.z[kk] = zz;
-      v[0] += (double)rr.x * zz.x + (double)rr.y * zz.y;
-      v[1] += (double)rr.x * rr.x + (double)rr.y * rr.y;
-    }
-  }
-  write_partials<2>(v, a.part + PCG_MAX_BLOCKS, lds);
-}
-
-// after the last enqueued iteration: record the final state for the host
-__global__ __launch_bounds__(256) void k_pcg_final(PcgArgs a, int k) {
-  __shared__ double lds[32];
-  if (a.st->done) return;
-  double sums[2];
-  prologue_sum<2>(sums, a.part + PCG_MAX_BLOCKS, a.nb, lds);
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
-    a.st->rr = sums[1];
-    a.st->iter = k;
-    a.st->done = sqrt(sums[1]) < a.st->atol ? 1 : 2;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Fused CG iteration: one launch per iteration (k_pcg_iter).  Launch K_k
 //   r_k = r_{k-1} - alpha_{k-1} q_{k-1},  x_k = x_{k-1} + alpha_{k-1} p_{k-1},
