@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # algorithmic bytes per pixel of each kernel's compulsory I/O (DESIGN.md
 # "Kernels and rooflines"); fp32 = 4 B, float2 = 8 B, planes counted once
 KERNEL_BYTES_PER_PX = {
-    "pcg_iter": 4 * 8 + 28 + 4 * 8,        # fused CG iteration: r, q, p, x + 7 coef planes -> r, p, q, x
+    "pcg_iter": 8 + 8 + 8 + 28 + 3 * 8,    # fused CG iteration: r, x, p_old + 7 coef planes -> r, x, p_new
     "flow_operator": 8 + 12 + 28 + 8,      # uv, It/Ix/Iy -> 7 coef + rhs
     "partial_deriv_hermite": 8 + 4 * 4 + 3 * 4 + 12,  # uv, I2/DX/DY/DXY, I1/I1x/I1y -> It/Ix/Iy
     "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ
@@ -150,33 +150,37 @@ def load_pmc_traffic(kernel, which="finest"):
 
 
 def roofline_of(ktimes, per_level):
-    """Roofline of the dominant HBM kernel.  Top level: every launch of the
-    kernel in the timed steps (algorithmic bytes = bytes/px x the launch's
-    level pixels; duration = HIP events on the ctx stream), which is what
-    the rocprofv3 --stats average of the same kernel measures.  `finest`:
-    the same restricted to the largest level's launches."""
+    """Roofline of the dominant HBM kernel.  Algorithmic bytes = bytes/px x
+    the level pixels of every launch that did work ("<name>.active" entries
+    from the library: CG launches enqueued after convergence return after
+    the prologue and move no data); time = HIP events on the ctx stream
+    around EVERY launch of the kernel, no-op ones included, so the figure is
+    conservative.  Top level: all levels (what the rocprofv3 --stats average
+    of the kernel covers); `finest`: the largest level only."""
     hbm = {k: v for k, v in ktimes.items() if k in KERNEL_BYTES_PER_PX}
     if not hbm:
         return None
     dom = max(hbm, key=lambda k: hbm[k]["ms_total"])
+    act = dom + ".active"
 
-    def fig(rec):
-        px_per_launch = rec["px"] / rec["launches"]
-        avg_ms = rec["ms_total"] / rec["launches"]
+    def fig(rec, arec):
+        work = arec if arec and arec["launches"] else rec
+        px_per_launch = work["px"] / work["launches"]
+        avg_ms = rec["ms_total"] / work["launches"]
         ach = KERNEL_BYTES_PER_PX[dom] * px_per_launch / (avg_ms * 1e-3) / 1e9
-        return round(ach, 1), round(avg_ms, 5), int(px_per_launch)
+        return round(ach, 1), round(avg_ms, 5), int(px_per_launch), work["launches"]
 
-    ach, avg_ms, ppl = fig(hbm[dom])
+    ach, avg_ms, ppl, nact = fig(hbm[dom], ktimes.get(act))
     out = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, "all"),
            "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": avg_ms, "px_per_launch": ppl,
-           "launches_per_step": hbm[dom]["launches"]}
+           "launches_per_step": hbm[dom]["launches"], "active_launches_per_step": nact}
     lv = [(px, rec) for (n, px), rec in per_level.items() if n == dom]
     if lv:
         px, rec = max(lv, key=lambda t: t[0])
-        a2, m2, p2 = fig(rec)
+        a2, m2, p2, n2 = fig(rec, per_level.get((act, px)))
         out["finest"] = {"px_per_launch": p2, "achieved": a2, "frac": round(a2 / HBM_PEAK_GBS, 4),
-                         "mean_launch_ms": m2, "launches_per_step": rec["launches"],
+                         "mean_launch_ms": m2, "launches_per_step": rec["launches"], "active_launches_per_step": n2,
                          "traffic": load_pmc_traffic(dom, "finest")}
     return out
 
@@ -235,6 +239,7 @@ def main():
 
     roofline = None
     ktimes = {}
+    pcg_levels = None
     if not args.no_profile:
         # profiled replay of the timed steps: HIP events around every launch
         # on the ctx stream (the stream the kernels run on)
@@ -257,6 +262,9 @@ def main():
             for k in agg:
                 agg[k] += rec[k]
         roofline = roofline_of(ktimes, per_level)
+        pcg_levels = [{"px": px, "ms": round(rec["ms_total"] / args.pairs, 3), "launches": rec["launches"] / args.pairs,
+                       "active": per_level.get(("pcg_iter.active", px), {}).get("launches", 0) / args.pairs}
+                      for (n, px), rec in sorted(per_level.items(), key=lambda kv: -kv[0][1]) if n == "pcg_iter"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -276,8 +284,10 @@ def main():
                              for l in sd["levels"]],
             "aepe_gt": round(aepe, 5), "solver_iters_total": sd["solver_iters_total"],
             "solver_iters_max": sd["solver_iters_max"], "solves": sd["solves"],
+            "pcg_per_level": pcg_levels,
             "kernel_ms_per_pair": {k: round(v["ms_total"] / args.pairs, 3) for k, v in
-                                   sorted(ktimes.items(), key=lambda kv: -kv[1]["ms_total"])[:12]},
+                                   sorted(ktimes.items(), key=lambda kv: -kv[1]["ms_total"])[:12]
+                                   if not k.endswith(".active")},
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

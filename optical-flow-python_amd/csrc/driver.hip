@@ -117,6 +117,7 @@ struct of_ctx {
   size_t tev_used = 0;
   std::vector<ProfRec> pending;
   std::map<std::string, KTime> ktimes;
+  std::map<int64_t, int> iter_hints;  // (H, W, solver) -> last iteration count
   double cur_px = 0;  // pixels processed by the launches being issued (profiling)
   std::vector<Slot> slots;
   ncclComm_t comm = nullptr;
@@ -459,11 +460,15 @@ Grid2 pair_grid(int H, int W) {
   return g;
 }
 
-// enqueue iterations in growing chunks; check the previous chunk's state
-// (pinned, double-buffered) while the current one runs
+// Enqueue iterations in chunks and poll the previous chunk's state (pinned,
+// double-buffered) while the current one runs.  The first chunk is sized by
+// `first` (the iteration count of the last solve of the same size and
+// solver, when known), the second is short, later ones grow up to
+// `max_chunk`: launches enqueued after convergence (cheap no-ops, but not
+// free) stay few without leaving the GPU idle while the host polls.
 template <typename Enq>
-int run_chunked(of_ctx *c, int maxiter, int first_chunk, int max_chunk, Enq enqueue_iter) {
-  int enq = 0, chunk = first_chunk, nchunks = 0;
+int run_chunked(of_ctx *c, int maxiter, int first, int max_chunk, Enq enqueue_iter) {
+  int enq = 0, chunk = first, nchunks = 0;
   while (enq < maxiter) {
     const int n = std::min(chunk, maxiter - enq);
     for (int t = 0; t < n; ++t) enqueue_iter(enq + t);
@@ -476,9 +481,24 @@ int run_chunked(of_ctx *c, int maxiter, int first_chunk, int max_chunk, Enq enqu
       HIPCHK(hipEventSynchronize(c->ev_state[slot ^ 1]));
       if (c->h_state[slot ^ 1].done) break;
     }
-    chunk = std::min(chunk * 2, max_chunk);
+    chunk = nchunks == 1 ? 4 : std::min(std::max(chunk + chunk / 2, 8), max_chunk);
   }
   return enq;
+}
+
+// iteration-count hint of the last solve with this size and solver
+int& iter_hint(of_ctx *c, int H, int W, int solver) {
+  return c->iter_hints[((int64_t)H << 32) | ((int64_t)W << 8) | solver];
+}
+
+// profiling: launches of a solve that did work (the rest returned after the
+// prologue); bench.py prices algorithmic bytes on these
+void note_active(of_ctx *c, const char *name, int launches, double px) {
+  if (!c->prof) return;
+  const std::string key = std::string(name) + ".active";
+  auto &s = c->ktimes[c->prof == 2 ? key + "@" + std::to_string((long long)px) : key];
+  s.px += launches * px;
+  s.n += launches;
 }
 
 SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
@@ -490,8 +510,12 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     const bool block = solver == OF_SOLVER_BACKSLASH;
     // fused-iteration geometry: 128-column strips x bands of R rows, 4 bands
     // per block, <= PCG_MAX_BLOCKS blocks, ~2048 waves when the level allows
-    const int nstrips = (W + 127) / 128;
-    int nbands = std::max(1, std::min((H + 3) / 4, 2048 / nstrips));
+    // fused-iteration geometry: PCG_SW-column strips x bands of R rows, 4
+    // bands per block, <= PCG_MAX_BLOCKS blocks, ~768 waves when the level
+    // allows (measured optimum at 1080p: fewer waves = less halo recompute,
+    // more = more latency hiding)
+    const int nstrips = (W + PCG_SW - 1) / PCG_SW;
+    int nbands = std::max(1, std::min((H + 3) / 4, 768 / nstrips));
     int R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
     int gyb = (nbands + 3) / 4;
@@ -506,8 +530,7 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     a.coef = coef.p;
     a.x = x.p;
     a.b = b.p;
-    F2 rb[2] = {new_f2(c, H, W), new_f2(c, H, W)}, qb[2] = {new_f2(c, H, W), new_f2(c, H, W)},
-       pb[2] = {new_f2(c, H, W), new_f2(c, H, W)};
+    F2 rb[2] = {new_f2(c, H, W), new_f2(c, H, W)}, pb[2] = {new_f2(c, H, W), new_f2(c, H, W)};
     a.H = H;
     a.W = W;
     a.P = b.P;
@@ -522,21 +545,26 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       PcgArgs ak = a;
       const int cur = k & 1, prev = cur ^ 1;
       ak.r_in = rb[prev].p;
-      ak.q_in = qb[prev].p;
       ak.p_old = pb[prev].p;
       ak.r_out = rb[cur].p;
-      ak.q_out = qb[cur].p;
       ak.p_new = pb[cur].p;
       return ak;
     };
-    const int enq = run_chunked(c, a.maxiter + 1, 8, 32, [&](int k) {
-      if (block) launch(c, "pcg_iter", k_pcg_iter<true>, grid, blk, 0, args_k(k), k, R, nbands);
-      else launch(c, "pcg_iter", k_pcg_iter<false>, grid, blk, 0, args_k(k), k, R, nbands);
+    int &hint = iter_hint(c, H, W, solver);
+    const int enq = run_chunked(c, a.maxiter + 1, hint > 0 ? std::max(8, hint * 3 / 4) : 8, 32, [&](int k) {
+      const bool odd = W & 1;
+      auto kern = k == 0 ? (block ? (odd ? k_cg<true, true, true> : k_cg<true, true, false>)
+                                  : (odd ? k_cg<true, false, true> : k_cg<true, false, false>))
+                         : (block ? (odd ? k_cg<false, true, true> : k_cg<false, true, false>)
+                                  : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
+      launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
     HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const PcgState &s = c->h_state[0];
+    hint = s.iter;
+    note_active(c, "pcg_iter", s.iter + 1, (double)H * W);
     return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
   }
   // red-black block SOR
@@ -556,7 +584,8 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
   a.tol = (float)P->sor_tol;
   a.maxiter = P->sor_max_iters;
   launch(c, "sor_init", k_sor_init, g.grid, g.block, 0, a);
-  const int enq = run_chunked(c, a.maxiter, 16, 64, [&](int k) {
+  int &hint = iter_hint(c, H, W, solver);
+  const int enq = run_chunked(c, a.maxiter, hint > 0 ? std::max(16, hint * 3 / 4) : 16, 64, [&](int k) {
     launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 0, k);
     launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 1, k);
   });
@@ -564,6 +593,7 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
   HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   const PcgState &s = c->h_state[0];
+  hint = s.iter;
   return {s.iter, s.done, 0.0};
 }
 

@@ -3,21 +3,13 @@
 // scipy.sparse.linalg.cg (x0 = 0, stop when ||r|| < rtol ||b|| before an
 // iteration, at most maxiter iterations), and red-black block SOR.
 //
-// One CG iteration = two launches; each global reduction is finished in the
-// PROLOGUE of the next launch (the launch-boundary reduce): every block of
-// the consumer sums the producer's per-block partials in the same fixed
-// order, so all blocks derive bit-identical scalars and no agent-scope
-// fence or atomic is needed (kernel boundaries give visibility).
-//
-//   spmv(k)   prologue: (k > 0) rz, rr of update(k-1) -> convergence test,
-//             beta = rz / rho[k-1]; body: p = z + beta p_old, q = A p,
-//             per-block p.q
-//   update(k) prologue: pq of spmv(k) -> alpha = rho[k] / pq; body:
-//             x += alpha p, r -= alpha q, z = M^-1 r, per-block r.z, r.r
-//
-// Kernels of a finished solve return at entry, so the host can enqueue
-// iterations in chunks.  Each thread owns two horizontally adjacent pixels
-// (8-B loads of scalar planes, 16-B loads of float2 fields).
+// CG: ONE launch per iteration (k_cg, below).  Every global reduction is
+// finished in the PROLOGUE of the next launch (launch-boundary reduce): each
+// block of the consumer sums the producer's per-block partials in the same
+// fixed order, so all blocks derive bit-identical scalars, and no
+// agent-scope fence or atomic is needed (kernel boundaries give visibility).
+// Launches of a finished solve return after the prologue, so the host can
+// enqueue iterations in chunks and poll a pinned status word.
 #include "kernels.h"
 
 #define PCG_MAX_BLOCKS 512
@@ -80,17 +72,11 @@ __device__ __forceinline__ void write_partials(double (&v)[NV], double *part, do
   }
 }
 
-// two-pixel loop: thread (tx, ty) of block (bx, by) owns columns
-// j0 = 2 * (bx * 64 + tx), j0 + 1 of rows by*4+ty, + gridDim.y*4, ...
-#define OF_FOR_PIXEL_PAIRS(H, W)                                         \
-  const int j0 = 2 * (blockIdx.x * OF_BX + threadIdx.x);                 \
-  for (int i = blockIdx.y * OF_BY + threadIdx.y; i < (H); i += gridDim.y * OF_BY)
-
 struct PcgArgs {
   const float *coef;  // 7 planes, plane stride ps
-  float2 *x, *r, *z, *p_old, *p_new, *q;
-  const float2 *r_in, *q_in;  // fused iteration: iterate k-1
-  float2 *r_out, *q_out;      // fused iteration: iterate k
+  float2 *x;
+  const float2 *r_in, *p_old;  // iterate k-1
+  float2 *r_out, *p_new;       // iterate k
   const float2 *b;
   int H, W, P;
   size_t ps;
@@ -100,48 +86,6 @@ struct PcgArgs {
   double rtol;
   int maxiter;
 };
-
-// ---------------------------------------------------------------------------
-// Fused CG iteration: one launch per iteration (k_pcg_iter).  Launch K_k
-//   r_k = r_{k-1} - alpha_{k-1} q_{k-1},  x_k = x_{k-1} + alpha_{k-1} p_{k-1},
-//   z_k = M^-1 r_k,  p_k = z_k + beta_k p_{k-1},  q_k = A p_k
-// and per-block sums S = (p.q, q.z, q.M^-1 q, r.z, r.r) of iterate k.  The
-// prologue of K_{k+1} turns the sums of K_k into
-//   alpha_k = (r.z)_k / (p.q)_k,  rho_{k+1} = (r.z)_k - 2 alpha_k (q.z)_k
-//   + alpha_k^2 (q.M^-1 q)_k (exact CG algebra), beta_{k+1} = rho_{k+1}/(r.z)_k
-// and applies scipy's test ||r_k|| < rtol ||b|| before iteration k.
-//
-// Geometry: a wave owns a 128-column strip (2 px per lane) and sweeps a band
-// of R rows top to bottom with a 3-row window in registers, so r, z, p of
-// every pixel are formed once; left/right neighbours come from the adjacent
-// lanes (DPP/bpermute), only lanes 0 and 63 reload the pixel across the
-// strip edge.  A block = 4 waves = 4 consecutive bands of one strip.
-struct PixIn {  // what a row load produces for one pixel
-  float2 r, z, p, pold;
-  float a, c, d;
-};
-
-template <bool BLOCK>
-__device__ __forceinline__ PixIn load_pix(const PcgArgs &g, int k, float alpha, float beta, size_t kk) {
-  PixIn v;
-  v.a = g.coef[4 * g.ps + kk];
-  v.c = g.coef[5 * g.ps + kk];
-  v.d = g.coef[6 * g.ps + kk];
-  if (k == 0) {
-    v.r = g.b[kk];
-    v.pold = make_float2(0.f, 0.f);
-  } else {
-    const float2 ro = g.r_in[kk], qo = g.q_in[kk];
-    v.r = make_float2(ro.x - alpha * qo.x, ro.y - alpha * qo.y);
-    v.pold = g.p_old[kk];
-  }
-  v.z = precond<BLOCK>(v.a, v.c, v.d, v.r);
-  v.p = k == 0 ? v.z : make_float2(v.z.x + beta * v.pold.x, v.z.y + beta * v.pold.y);
-  return v;
-}
-
-__device__ __forceinline__ float shfl_up1(float v) { return __shfl_up(v, 1, 64); }
-__device__ __forceinline__ float shfl_dn1(float v) { return __shfl_down(v, 1, 64); }
 
 // the shared prologue: returns 1 when the solve is finished (state written)
 __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds, float *alpha, float *beta) {
@@ -176,104 +120,305 @@ __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds
   return s_exit;
 }
 
+// ---------------------------------------------------------------------------
+// q-free fused CG iteration on raw buffer loads (k_cg): the production CG
+// kernel.  Same algebra as k_pcg_iter (rho recurrence, launch-boundary
+// reduction), but
+//  - q_{k-1} = A p_{k-1} is recomputed from p_{k-1} (read anyway, 2-row
+//    halo) instead of being stored and re-read: 76 B/px per iteration
+//    (r, x read+write; p_old read; p_new write; 7 coefficient planes);
+//  - every load is a raw buffer load whose out-of-image offsets (rows outside
+//    [0, H), columns outside [0, W)) return 0 by the hardware range check, so
+//    the stencil needs no boundary branches, and stores from halo lanes are
+//    dropped the same way;
+//  - the first iteration and the 2x2 block / scalar Jacobi choice are
+//    template parameters; dot products are formed per lane in fp32 over the
+//    lane's two pixels and accumulated in fp64;
+//  - the launch prologue issues the partial-sum loads, the state loads and
+//    the first pipeline rows together (one memory round trip, not four).
+// Geometry: a wave owns PCG_SW = 124 output columns; lane l holds columns
+// jc = j0 - 2 + 2l and jc + 1, so lanes 0 and 63 carry the strip halo and all
+// horizontal neighbours are DPP wave shifts.  A band of R rows is swept top
+// to bottom; step t prefetches row t+1 (coefficients, r_in) and p_old of row
+// t+2, forms r, z, p of row t and finishes row t-1 (q = A p, stores, dots).
+#define PCG_SW 124
+#define CG_OOB 0x80000000u
+
+typedef float cg_f2 __attribute__((ext_vector_type(2)));
+typedef float cg_f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cg_rsrc(const void *p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)min(bytes, (size_t)0x7fffffff), 0x00020000);
+}
+__device__ __forceinline__ cg_f2 cg_ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(cg_f2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ cg_f4 cg_ld4(__amdgpu_buffer_rsrc_t r, unsigned voff) {
+  return __builtin_bit_cast(cg_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
+}
+__device__ __forceinline__ void cg_st4(__amdgpu_buffer_rsrc_t r, unsigned voff, cg_f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v), r, (int)voff,
+                                         0, 0);
+}
+// lane l <- lane l-1 (wave_shr:1) and lane l <- lane l+1 (wave_shl:1); lanes
+// without a source read 0 (bound_ctrl)
+__device__ __forceinline__ float cg_from_left(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float cg_from_right(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+
+struct CgCoef {  // one row, the lane's two pixels (x: first, y: second)
+  cg_f2 wxu, wyu, wxv, wyv, a, c, d;
+  float wlu, wlv;  // weight of the edge to the left of the first pixel
+};
+
+template <bool ODD>
+__device__ __forceinline__ cg_f2 cg_mask1(cg_f2 v, bool ok1) {
+  if (ODD && !ok1) v.y = 0.f;
+  return v;
+}
+template <bool ODD>
+__device__ __forceinline__ cg_f4 cg_mask1(cg_f4 v, bool ok1) {
+  if (ODD && !ok1) { v.z = 0.f; v.w = 0.f; }
+  return v;
+}
+
+// (A f)(row) for f = (u0, v0, u1, v1) rows up / mid / dn; wu = vertical
+// weights of the row above (u: .x/.y = pixel 0/1 of wyu, v likewise)
+__device__ __forceinline__ cg_f4 cg_apply(cg_f4 up, cg_f4 mid, cg_f4 dn, const CgCoef &c, cg_f2 wuu, cg_f2 wuv) {
+  const float Lu = cg_from_left(mid.z), Lv = cg_from_left(mid.w);
+  const float Ru = cg_from_right(mid.x), Rv = cg_from_right(mid.y);
+  const float s0u = c.wlu * Lu + c.wxu.x * mid.z + wuu.x * up.x + c.wyu.x * dn.x;
+  const float s0v = c.wlv * Lv + c.wxv.x * mid.w + wuv.x * up.y + c.wyv.x * dn.y;
+  const float s1u = c.wxu.x * mid.x + c.wxu.y * Ru + wuu.y * up.z + c.wyu.y * dn.z;
+  const float s1v = c.wxv.x * mid.y + c.wxv.y * Rv + wuv.y * up.w + c.wyv.y * dn.w;
+  cg_f4 o;
+  o.x = c.a.x * mid.x + c.c.x * mid.y - s0u;
+  o.y = c.c.x * mid.x + c.d.x * mid.y - s0v;
+  o.z = c.a.y * mid.z + c.c.y * mid.w - s1u;
+  o.w = c.c.y * mid.z + c.d.y * mid.w - s1v;
+  return o;
+}
+
+// inverse of the preconditioner block of both pixels: (ia, ic, id) with
+// M^-1 (ru, rv) = (ia ru + ic rv, ic ru + id rv)
+struct CgInv {
+  cg_f2 ia, ic, id;
+};
 template <bool BLOCK>
-__global__ __launch_bounds__(256) void k_pcg_iter(PcgArgs g, int k, int R, int nbands) {
-  __shared__ double lds[64];
-  if (g.st->done) return;
-  float alpha = 0.f, beta = 0.f;
-  if (k >= 1 && pcg_prologue(g, k, lds, &alpha, &beta)) return;
-  if (k == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
-    g.st->iter = 0;
-    g.st->maxiter = g.maxiter;
-  }
-  const int H = g.H, W = g.W, P = g.P;
-  const int lane = threadIdx.x, band = blockIdx.y * 4 + threadIdx.y;
-  const int j0 = blockIdx.x * 128 + 2 * lane;
-  const bool v0 = j0 < W, v1 = j0 + 1 < W;
-  const float *wxu = g.coef, *wyu = g.coef + g.ps, *wxv = g.coef + 2 * g.ps, *wyv = g.coef + 3 * g.ps;
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (band < nbands) {
-    const int r0 = band * R, r1 = min(r0 + R, H);
-    auto load_row = [&](int ii, PixIn &e0, PixIn &e1) {
-      const bool ok = ii >= 0 && ii < H;
-      const size_t kk = (size_t)ii * P + j0;
-      if (ok && v0) e0 = load_pix<BLOCK>(g, k, alpha, beta, kk);
-      else e0.p = make_float2(0.f, 0.f);
-      if (ok && v1) e1 = load_pix<BLOCK>(g, k, alpha, beta, kk + 1);
-      else e1.p = make_float2(0.f, 0.f);
-    };
-    auto p_at = [&](int ii, int jj) -> float2 {  // strip-edge neighbour
-      if (jj < 0 || jj >= W) return make_float2(0.f, 0.f);
-      return load_pix<BLOCK>(g, k, alpha, beta, (size_t)ii * P + jj).p;
-    };
-    PixIn m0, m1, c0, c1, n0, n1;
-    load_row(r0 - 1, m0, m1);
-    load_row(r0, c0, c1);
-    float2 wyu_up = make_float2(0.f, 0.f), wyv_up = wyu_up;  // edge weights row i-1 -> i
-    if (r0 > 0) {
-      const size_t ku = (size_t)(r0 - 1) * P + j0;
-      if (v0) { wyu_up.x = wyu[ku]; wyv_up.x = wyv[ku]; }
-      if (v1) { wyu_up.y = wyu[ku + 1]; wyv_up.y = wyv[ku + 1]; }
-    }
-    for (int i = r0; i < r1; ++i) {
-      load_row(i + 1, n0, n1);
-      const size_t kk = (size_t)i * P + j0;
-      // horizontal neighbours of the pair: lane-1's second pixel, lane+1's first
-      float2 L = make_float2(shfl_up1(c1.p.x), shfl_up1(c1.p.y));
-      float2 Rn = make_float2(shfl_dn1(c0.p.x), shfl_dn1(c0.p.y));
-      float wx0u = v0 ? wxu[kk] : 0.f, wx0v = v0 ? wxv[kk] : 0.f;
-      float wx1u = v1 ? wxu[kk + 1] : 0.f, wx1v = v1 ? wxv[kk + 1] : 0.f;
-      float wLu = shfl_up1(wx1u), wLv = shfl_up1(wx1v);
-      if (lane == 0) {
-        L = p_at(i, j0 - 1);
-        wLu = j0 > 0 ? wxu[kk - 1] : 0.f;
-        wLv = j0 > 0 ? wxv[kk - 1] : 0.f;
-      }
-      if (lane == 63) Rn = p_at(i, j0 + 2);
-      float2 wyu_dn = make_float2(0.f, 0.f), wyv_dn = wyu_dn;
-      if (i < H - 1) {
-        if (v0) { wyu_dn.x = wyu[kk]; wyv_dn.x = wyv[kk]; }
-        if (v1) { wyu_dn.y = wyu[kk + 1]; wyv_dn.y = wyv[kk + 1]; }
-      }
+__device__ __forceinline__ CgInv cg_inv(const CgCoef &c) {
+  CgInv o;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const bool valid = e ? v1 : v0;
-        if (!valid) continue;
-        const int j = j0 + e;
-        const PixIn &c = e ? c1 : c0;
-        const float2 left = e ? c0.p : L, right = e ? Rn : c1.p;
-        const float wl_u = e ? wx0u : wLu, wl_v = e ? wx0v : wLv;
-        const float wr_u = e ? wx1u : wx0u, wr_v = e ? wx1v : wx0v;
-        const float2 up = e ? m1.p : m0.p, dn = e ? n1.p : n0.p;
-        const float wu_u = e ? wyu_up.y : wyu_up.x, wu_v = e ? wyv_up.y : wyv_up.x;
-        const float wd_u = e ? wyu_dn.y : wyu_dn.x, wd_v = e ? wyv_dn.y : wyv_dn.x;
-        float su = 0.f, sv = 0.f;
-        if (j < W - 1) { su += wr_u * right.x; sv += wr_v * right.y; }
-        if (j > 0) { su += wl_u * left.x; sv += wl_v * left.y; }
-        if (i < H - 1) { su += wd_u * dn.x; sv += wd_v * dn.y; }
-        if (i > 0) { su += wu_u * up.x; sv += wu_v * up.y; }
-        const float2 q = make_float2(c.a * c.p.x + c.c * c.p.y - su, c.c * c.p.x + c.d * c.p.y - sv);
-        const size_t kj = kk + e;
-        g.r_out[kj] = c.r;
-        g.p_new[kj] = c.p;
-        g.q_out[kj] = q;
-        if (k == 0) g.x[kj] = make_float2(0.f, 0.f);
-        else {
-          float2 xx = g.x[kj];
-          xx.x += alpha * c.pold.x;
-          xx.y += alpha * c.pold.y;
-          g.x[kj] = xx;
-        }
-        const float2 mq = precond<BLOCK>(c.a, c.c, c.d, q);
-        acc[0] += (double)c.p.x * q.x + (double)c.p.y * q.y;
-        acc[1] += (double)q.x * c.z.x + (double)q.y * c.z.y;
-        acc[2] += (double)q.x * mq.x + (double)q.y * mq.y;
-        acc[3] += (double)c.r.x * c.z.x + (double)c.r.y * c.z.y;
-        acc[4] += (double)c.r.x * c.r.x + (double)c.r.y * c.r.y;
+  for (int e = 0; e < 2; ++e) {
+    const float a = c.a[e], cc = c.c[e], d = c.d[e];
+    // scalar Jacobi, base.py:129-131: 1/diag where |diag| > 1e-12 else 0
+    float ia = fabsf(a) > 1e-12f ? __builtin_amdgcn_rcpf(a) : 0.f;
+    float id = fabsf(d) > 1e-12f ? __builtin_amdgcn_rcpf(d) : 0.f;
+    float ic = 0.f;
+    if (BLOCK) {
+      const float det = a * d - cc * cc;
+      const bool ok = det > 1e-30f * fabsf(a * d);
+      const float inv = __builtin_amdgcn_rcpf(det);
+      ia = ok ? d * inv : ia;
+      id = ok ? a * inv : id;
+      ic = ok ? -cc * inv : 0.f;
+    }
+    o.ia[e] = ia;
+    o.ic[e] = ic;
+    o.id[e] = id;
+  }
+  return o;
+}
+__device__ __forceinline__ cg_f4 cg_minv(const CgInv &m, cg_f4 r) {
+  cg_f4 z;
+  z.x = m.ia.x * r.x + m.ic.x * r.y;
+  z.y = m.ic.x * r.x + m.id.x * r.y;
+  z.z = m.ia.y * r.z + m.ic.y * r.w;
+  z.w = m.ic.y * r.z + m.id.y * r.w;
+  return z;
+}
+__device__ __forceinline__ float cg_dot(cg_f4 a, cg_f4 b) { return a.x * b.x + a.y * b.y + (a.z * b.z + a.w * b.w); }
+
+template <bool FIRST, bool BLOCK, bool ODD>
+__global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands) {
+  __shared__ double lds[64];
+  __shared__ int s_exit;
+  __shared__ float s_ab[2];
+  const int H = g.H, W = g.W;
+  const unsigned rowb4 = (unsigned)g.P * 4u, rowb8 = (unsigned)g.P * 8u;
+  const size_t vbytes = (size_t)H * g.P * 8;
+  const __amdgpu_buffer_rsrc_t rc = cg_rsrc(g.coef, g.ps * 7 * 4);
+  const __amdgpu_buffer_rsrc_t rin = cg_rsrc(FIRST ? g.b : g.r_in, vbytes);
+  const __amdgpu_buffer_rsrc_t rpo = cg_rsrc(g.p_old, vbytes);
+  const __amdgpu_buffer_rsrc_t rx = cg_rsrc(g.x, vbytes);
+  const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
+  const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
+  const unsigned ps4 = (unsigned)(g.ps * 4);
+  const int lane = threadIdx.x, band = blockIdx.y * 4 + threadIdx.y;
+  const int jc = blockIdx.x * PCG_SW - 2 + 2 * lane;
+  const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
+  const bool out_lane = lane >= 1 && lane <= 62;
+  const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
+  const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
+  const bool live = band < nbands;
+  const int r0 = band * R, r1 = min(r0 + R, H);
+
+  auto o4 = [&](int t) { return (unsigned)t < (unsigned)H ? off4 + (unsigned)t * rowb4 : CG_OOB; };
+  auto o8 = [&](int t) { return (unsigned)t < (unsigned)H ? off8 + (unsigned)t * rowb8 : CG_OOB; };
+  auto load_coef = [&](int t, CgCoef &c) {
+    const unsigned v = o4(t);
+    c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
+    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
+    c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
+    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
+    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
+    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
+    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
+  };
+  auto load_wy = [&](int t, cg_f2 &wu, cg_f2 &wv) {
+    const unsigned v = o4(t);
+    wu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
+    wv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
+  };
+  auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
+  auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
+
+  // ---- pipeline preamble (independent of alpha/beta: issued before the
+  // prologue's reduction so the two memory round trips overlap).  Rows live
+  // in 4-slot register rings indexed by (row - (r0 - 1)) & 3, and the row
+  // loop is unrolled by 4, so the pipeline advances without register moves.
+  CgCoef C[4];   // coefficients, rows t-2 (vertical weights only) .. t+1
+  cg_f4 PO[4];   // p_old, rows t-1 .. t+2
+  cg_f4 RI[2];   // r_in, rows t, t+1
+  if (live) {
+    const int t = r0 - 1;
+    load_wy(t - 2, C[2].wyu, C[2].wyv);
+    load_coef(t - 1, C[3]);
+    load_coef(t, C[0]);
+    PO[3] = load_po(t - 1);
+    PO[0] = load_po(t);
+    PO[1] = load_po(t + 1);
+    RI[0] = load_rin(t);
+  }
+
+  // ---- prologue: alpha_{k-1}, beta_k and the convergence test
+  float alpha = 0.f, beta = 0.f;
+  {
+    const int tid = threadIdx.x + threadIdx.y * 64;
+    int st_done = 0;
+    double st_atol = 0.0;
+    if (tid == 0) {
+      st_done = g.st->done;
+      st_atol = g.st->atol;
+    }
+    double S[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (!FIRST) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        double s = 0.0;
+        for (int b = tid; b < g.nb; b += 256) s += g.part[(size_t)v * PCG_MAX_BLOCKS + b];
+        S[v] = wave_sum(s);
       }
-      m0 = c0; m1 = c1; c0 = n0; c1 = n1;
-      wyu_up = wyu_dn;
-      wyv_up = wyv_dn;
+      if ((tid & 63) == 0)
+#pragma unroll
+        for (int v = 0; v < 5; ++v) lds[v * 8 + (tid >> 6)] = S[v];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int done = st_done ? -1 : 0;
+      float al = 0.f, be = 0.f;
+      if (!FIRST && !done) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) S[v] = lds[v * 8] + lds[v * 8 + 1] + lds[v * 8 + 2] + lds[v * 8 + 3];
+        const double rn = sqrt(S[4]);
+        const double atol = k == 1 ? g.rtol * rn : st_atol;
+        if (k == 1 && S[4] == 0.0) done = 3;
+        else if (rn < atol) done = 1;
+        else if (k - 1 >= g.maxiter) done = 2;
+        const double a_ = S[3] / S[0];
+        const double rho = S[3] - 2.0 * a_ * S[1] + a_ * a_ * S[2];
+        if (blockIdx.x == 0 && blockIdx.y == 0) {
+          if (k == 1) { g.st->bnorm = rn; g.st->atol = atol; }
+          g.st->iter = k - 1;
+          g.st->rr = S[4];
+          g.st->rho[k & 1] = rho;
+          if (done) g.st->done = done;
+        }
+        al = (float)a_;
+        be = (float)(rho / S[3]);
+      }
+      if (FIRST && blockIdx.x == 0 && blockIdx.y == 0) {
+        g.st->iter = 0;
+        g.st->maxiter = g.maxiter;
+      }
+      s_exit = done;
+      s_ab[0] = al;
+      s_ab[1] = be;
+    }
+    __syncthreads();
+    if (s_exit) return;
+    alpha = s_ab[0];
+    beta = s_ab[1];
+  }
+
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    cg_f4 PP[4] = {zero4, zero4, zero4, zero4};  // p, rows t-2 .. t
+    cg_f4 RR[2] = {zero4, zero4}, ZZ[2] = {zero4, zero4}, XX[2] = {zero4, zero4};  // rows t-1, t
+    CgInv MI[2];
+    C[3].wlu = cg_from_left(C[3].wxu.y);
+    C[3].wlv = cg_from_left(C[3].wxv.y);
+    MI[1] = cg_inv<BLOCK>(C[3]);
+    const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;  // pixels whose dots count
+    for (int t0 = r0 - 1; t0 <= r1; t0 += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u;
+        if (t > r1) break;
+        CgCoef &cm2 = C[(u + 2) & 3], &cm1 = C[(u + 3) & 3], &c0 = C[u & 3], &cp1 = C[(u + 1) & 3];
+        // prefetch: coefficients and r_in of row t+1, p_old of row t+2, x of row t
+        load_coef(t + 1, cp1);
+        RI[(u + 1) & 1] = load_rin(t + 1);
+        PO[(u + 2) & 3] = load_po(t + 2);
+        XX[u & 1] = (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : zero4;
+        // r, z, p of row t
+        c0.wlu = cg_from_left(c0.wxu.y);
+        c0.wlv = cg_from_left(c0.wxv.y);
+        MI[u & 1] = cg_inv<BLOCK>(c0);
+        cg_f4 r = RI[u & 1];
+        if (!FIRST) r -= alpha * cg_apply(PO[(u + 3) & 3], PO[u & 3], PO[(u + 1) & 3], c0, cm1.wyu, cm1.wyv);
+        const cg_f4 z = cg_minv(MI[u & 1], r);
+        cg_f4 p = FIRST ? z : z + beta * PO[u & 3];
+        const bool rv = (unsigned)t < (unsigned)H;
+        if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
+        if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
+        PP[u & 3] = p;
+        RR[u & 1] = r;
+        ZZ[u & 1] = z;
+        // finish row t-1
+        const int o = t - 1;
+        if (o >= r0) {
+          const cg_f4 pm1 = PP[(u + 3) & 3], rm1 = RR[(u + 1) & 1], zm1 = ZZ[(u + 1) & 1];
+          const cg_f4 q = cg_apply(PP[(u + 2) & 3], pm1, p, cm1, cm2.wyu, cm2.wyv);
+          const cg_f4 mq = cg_minv(MI[(u + 1) & 1], q);
+          const unsigned so = soff8 + (unsigned)o * rowb8;
+          cg_st4(rro, so, rm1);
+          cg_st4(rpn, so, pm1);
+          cg_st4(rx, so, FIRST ? zero4 : XX[(u + 1) & 1] + alpha * PO[(u + 3) & 3]);
+          // per-lane fp32 dots over the two pixels (halo lanes / padding masked)
+          cg_f4 qm = q, rm = rm1;  // select, not multiply: halo lanes may hold inf/nan
+          if (!dm0) { qm.x = 0.f; qm.y = 0.f; rm.x = 0.f; rm.y = 0.f; }
+          if (!dm1) { qm.z = 0.f; qm.w = 0.f; rm.z = 0.f; rm.w = 0.f; }
+          acc[0] += (double)cg_dot(pm1, qm);
+          acc[1] += (double)cg_dot(qm, zm1);
+          acc[2] += (double)cg_dot(qm, mq);
+          acc[3] += (double)cg_dot(rm, zm1);
+          acc[4] += (double)cg_dot(rm, rm1);
+        }
+      }
     }
   }
   write_partials<5>(acc, g.part, lds);

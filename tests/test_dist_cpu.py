@@ -79,6 +79,7 @@ def test_bench_single_process_defaults(monkeypatch):
 def test_roofline_of_all_and_finest():
     import bench
     per_level = {("pcg_iter", 1000): {"ms_total": 2.0, "launches": 10, "px": 1e10},
+                 ("pcg_iter.active", 1000): {"ms_total": 0.0, "launches": 8, "px": 8e9},
                  ("pcg_iter", 100): {"ms_total": 1.0, "launches": 10, "px": 1e9},
                  ("wmf", 1000): {"ms_total": 0.5, "launches": 1, "px": 1000.0}}
     kt = {}
@@ -89,6 +90,10 @@ def test_roofline_of_all_and_finest():
     r = bench.roofline_of(kt, per_level)
     bpp = bench.KERNEL_BYTES_PER_PX["pcg_iter"]
     assert r["kernel"] == "pcg_iter"
-    assert r["achieved"] == pytest.approx(bpp * 5.5e8 / 0.15e-3 / 1e9, rel=1e-3)
-    assert r["finest"]["achieved"] == pytest.approx(bpp * 1e9 / 0.2e-3 / 1e9, rel=1e-3)
+    # all levels: only the finest level reports active launches -> 8 launches
+    # of 1e9 px priced against the 3 ms of all 20 launches
+    assert r["achieved"] == pytest.approx(bpp * 1e9 / (3.0 / 8 * 1e-3) / 1e9, rel=1e-3)
+    # finest: 8 active launches of 1e9 px in 2 ms
+    assert r["finest"]["achieved"] == pytest.approx(bpp * 1e9 / (2.0 / 8 * 1e-3) / 1e9, rel=1e-3)
+    assert r["finest"]["active_launches_per_step"] == 8
     assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
