@@ -514,7 +514,10 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     // bands per block, <= PCG_MAX_BLOCKS blocks, ~768 waves when the level
     // allows (measured optimum at 1080p: fewer waves = less halo recompute,
     // more = more latency hiding)
-    const int nstrips = (W + PCG_SW - 1) / PCG_SW;
+    // 'backslash' runs the Neumann-preconditioned kernel (k_cgn, 120-column
+    // strips), 'pcg' scipy's Jacobi CG (k_cg, 124-column strips)
+    const int sw = block ? PCG_SWN : PCG_SW;
+    const int nstrips = (W + sw - 1) / sw;
     int nbands = std::max(1, std::min((H + 3) / 4, 768 / nstrips));
     int R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
@@ -553,9 +556,9 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     int &hint = iter_hint(c, H, W, solver);
     const int enq = run_chunked(c, a.maxiter + 1, hint > 0 ? std::max(8, hint * 3 / 4) : 8, 32, [&](int k) {
       const bool odd = W & 1;
-      auto kern = k == 0 ? (block ? (odd ? k_cg<true, true, true> : k_cg<true, true, false>)
-                                  : (odd ? k_cg<true, false, true> : k_cg<true, false, false>))
-                         : (block ? (odd ? k_cg<false, true, true> : k_cg<false, true, false>)
+      auto kern = block ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
+                                  : (odd ? k_cgn<false, true> : k_cgn<false, false>))
+                        : (k == 0 ? (odd ? k_cg<true, false, true> : k_cg<true, false, false>)
                                   : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
