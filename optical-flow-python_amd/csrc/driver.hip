@@ -12,7 +12,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <immintrin.h>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -107,6 +109,7 @@ struct of_ctx {
   Arena arena;
   PcgState *d_state = nullptr, *h_state = nullptr;  // h_state: 2 pinned slots
   hipEvent_t ev_state[2] = {nullptr, nullptr};
+  CgFlag *h_flag = nullptr, *d_flag = nullptr;  // mapped coherent host memory
   double *d_partials = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
@@ -486,6 +489,38 @@ int run_chunked(of_ctx *c, int maxiter, int first, int max_chunk, Enq enqueue_it
   return enq;
 }
 
+// Feed CG launches `depth` ahead of the progress the kernels report in the
+// mapped host flag; stop enqueueing as soon as a prologue has declared the
+// solve done.  Returns the number of launches enqueued.
+template <typename Enq>
+int run_fed(of_ctx *c, int nmax, int depth, Enq enqueue_iter) {
+  volatile CgFlag *f = c->h_flag;
+  f->done = 0;
+  f->iter = 0;
+  f->k = -1;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  int enq = 0;
+  while (enq < nmax) {
+    if (f->done) break;
+    if (enq - f->k <= depth) {
+      enqueue_iter(enq++);
+      continue;
+    }
+    // the GPU is `depth` launches behind: wait for progress (bounded: after
+    // 0.5 s drain the stream; the flag must then show every launch)
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!f->done && enq - f->k > depth) {
+      _mm_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        REQUIRE(f->done || f->k == enq - 1, OF_EHIP, "CG progress flag not visible to the host");
+        break;
+      }
+    }
+  }
+  return enq;
+}
+
 // iteration-count hint of the last solve with this size and solver
 int& iter_hint(of_ctx *c, int H, int W, int solver) {
   return c->iter_hints[((int64_t)H << 32) | ((int64_t)W << 8) | solver];
@@ -553,8 +588,8 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       ak.p_new = pb[cur].p;
       return ak;
     };
-    int &hint = iter_hint(c, H, W, solver);
-    const int enq = run_chunked(c, a.maxiter + 1, hint > 0 ? std::max(8, hint * 3 / 4) : 8, 32, [&](int k) {
+    a.hflag = c->d_flag;
+    const int enq = run_fed(c, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
       auto kern = block ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
                                   : (odd ? k_cgn<false, true> : k_cgn<false, false>))
@@ -566,7 +601,6 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const PcgState &s = c->h_state[0];
-    hint = s.iter;
     note_active(c, "pcg_iter", s.iter + 1, (double)H * W);
     return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
   }
@@ -989,6 +1023,8 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_state, sizeof(PcgState)));
     HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&c->h_flag, sizeof(CgFlag), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
     HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 8 * PCG_MAX_BLOCKS));
@@ -1021,6 +1057,7 @@ int of_ctx_destroy(of_ctx *c) {
     if (e) hipEventDestroy(e);
   hipFree(c->d_state);
   hipHostFree(c->h_state);
+  if (c->h_flag) hipHostFree(c->h_flag);
   hipFree(c->d_partials);
   hipFree(c->d_mm);
   hipFree(c->d_norm);

@@ -38,6 +38,16 @@ struct DerivArgs {
 };
 
 // PCG scalar state (device-resident; mirrored to pinned host memory)
+// CG progress mirrored to mapped, coherent host memory by the lead block of
+// every launch: the host feeds launches a few ahead of `k` and stops as soon
+// as `done` is set (no event round trip, few no-op launches)
+struct CgFlag {
+  int k;      // last launch whose prologue ran
+  int done;   // PcgState::done once decided
+  int iter;
+  int pad_;
+};
+
 struct PcgState {
   double rho[2];    // r.z of iterate k at rho[k & 1]
   double rr;        // r.r

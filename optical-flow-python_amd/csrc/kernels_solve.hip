@@ -83,6 +83,7 @@ struct PcgArgs {
   int nb;  // blocks of this grid (== blocks of every launch of the solve)
   double *part;  // [5][PCG_MAX_BLOCKS] partial sums (layout per kernel pair)
   PcgState *st;
+  CgFlag *hflag;  // mapped host memory (may be null)
   double rtol;
   int maxiter;
 };
@@ -295,6 +296,13 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
     if (FIRST && blockIdx.x == 0 && blockIdx.y == 0) {
       g.st->iter = 0;
       g.st->maxiter = g.maxiter;
+    }
+    if (g.hflag && blockIdx.x == 0 && blockIdx.y == 0 && done >= 0) {
+      if (done > 0) {
+        __hip_atomic_store(&g.hflag->iter, k - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&g.hflag->done, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __hip_atomic_store(&g.hflag->k, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     s_exit = done;
     s_ab[0] = al;
