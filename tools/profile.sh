@@ -11,7 +11,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-profile $*"
-KRE='pcg|wmf|flow_operator|partial_deriv|rof|minmax|update_occ|median|f2_to_planar'
+KRE='cg|wmf|flow_operator|partial_deriv|rof|minmax|update_occ|median|f2_to_planar'
 tools/gpu_step.sh 300 $OUT/trace.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace -- python3 $B || exit $?
 tools/gpu_step.sh 600 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $B || exit $?
 tools/gpu_step.sh 600 $OUT/write.log rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o write -- python3 $B || exit $?
