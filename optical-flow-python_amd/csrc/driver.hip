@@ -536,6 +536,50 @@ void note_active(of_ctx *c, const char *name, int launches, double px) {
   s.n += launches;
 }
 
+// Coefficients c_i of the degree-m polynomial preconditioner of k_cgp,
+// M^-1 = sum_i c_i B^i D^-1 with B = I - X, X = D^-1 A: the Chebyshev
+// residual polynomial 1 - X p(X) = T_{m+1}((b + a - 2X) / (b - a)) /
+// T_{m+1}((b + a) / (b - a)), re-expanded in powers of B.
+void cheb_poly(int m, double a, double b, double *cB) {
+  std::vector<std::vector<double>> T(m + 2);
+  T[0] = {1.0};
+  T[1] = {0.0, 1.0};
+  for (int i = 2; i <= m + 1; ++i) {
+    T[i].assign(i + 1, 0.0);
+    for (size_t j = 0; j < T[i - 1].size(); ++j) T[i][j + 1] += 2.0 * T[i - 1][j];
+    for (size_t j = 0; j < T[i - 2].size(); ++j) T[i][j] -= T[i - 2][j];
+  }
+  auto binom = [](int n, int k) {
+    double r = 1.0;
+    for (int i = 1; i <= k; ++i) r = r * (n - k + i) / i;
+    return r;
+  };
+  const double s = (b + a) / (b - a), g = -2.0 / (b - a);
+  const std::vector<double> &t = T[m + 1];
+  double Ts = 0.0;
+  for (int kk = 0; kk <= m + 1; ++kk) Ts += t[kk] * std::pow(s, kk);
+  std::vector<double> Rx(m + 2, 0.0);  // R(X) in powers of X
+  for (int kk = 0; kk <= m + 1; ++kk)
+    for (int j = 0; j <= kk; ++j) Rx[j] += t[kk] * binom(kk, j) * std::pow(s, kk - j) * std::pow(g, j) / Ts;
+  std::vector<double> pX(m + 1);  // p(X) = (1 - R(X)) / X
+  for (int j = 1; j <= m + 1; ++j) pX[j - 1] = -Rx[j];
+  for (int i = 0; i <= m; ++i) {  // p(1 - B)
+    double v = 0.0;
+    for (int j = i; j <= m; ++j) v += pX[j] * binom(j, i) * ((i & 1) ? -1.0 : 1.0);
+    cB[i] = v;
+  }
+}
+
+// 'backslash' CG kernel: 3 = Chebyshev degree-3 polynomial (k_cgp, default),
+// 1 = first-order Neumann (k_cgn); OF_CG_POLY overrides (A/B measurements)
+int cg_poly_degree() {
+  static int d = [] {
+    const char *e = getenv("OF_CG_POLY");
+    return e && atoi(e) == 1 ? 1 : 3;
+  }();
+  return d;
+}
+
 SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
   const int H = b.H, W = b.W;
   c->cur_px = (double)H * W;
@@ -551,13 +595,19 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     // more = more latency hiding)
     // 'backslash' runs the Neumann-preconditioned kernel (k_cgn, 120-column
     // strips), 'pcg' scipy's Jacobi CG (k_cg, 124-column strips)
-    const int sw = block ? PCG_SWN : PCG_SW;
+    const int deg = block ? cg_poly_degree() : 0;
+    const int sw = deg == 3 ? PCG_SWP : deg == 1 ? PCG_SWN : PCG_SW;
     const int nstrips = (W + sw - 1) / sw;
-    int nbands = std::max(1, std::min((H + 3) / 4, 768 / nstrips));
+    // waves per launch: k_cgp (1 wave per SIMD, LDS ring) fills all 256 CUs
+    static const int waves_env = getenv("OF_CG_WAVES") ? atoi(getenv("OF_CG_WAVES")) : 0;
+    const int waves = waves_env > 0 ? waves_env : (deg == 3 ? 1024 : 768);
+    REQUIRE(deg != 3 || coef.ps() * 7 * 4 < 0x40000000ull, OF_ENOTSUP, "level too large for the CG kernel");
+    int nbands = std::max(1, std::min((H + 3) / 4, waves / nstrips));
     int R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
     int gyb = (nbands + 3) / 4;
-    while (nstrips * gyb > PCG_MAX_BLOCKS) {
+    const int max_blocks = deg == 3 ? 256 : PCG_MAX_BLOCKS;  // k_cgp: one 128-KB-LDS block per CU
+    while (nstrips * gyb > max_blocks) {
       ++R;
       nbands = (H + R - 1) / R;
       gyb = (nbands + 3) / 4;
@@ -588,13 +638,20 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       ak.p_new = pb[cur].p;
       return ak;
     };
+    if (deg == 3) {
+      double cb[4];
+      cheb_poly(3, 0.04, 2.0, cb);
+      for (int i = 0; i < 4; ++i) a.poly[i] = (float)cb[i];
+    }
     a.hflag = c->d_flag;
     const int enq = run_fed(c, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
-      auto kern = block ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
-                                  : (odd ? k_cgn<false, true> : k_cgn<false, false>))
-                        : (k == 0 ? (odd ? k_cg<true, false, true> : k_cg<true, false, false>)
-                                  : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
+      auto kern = deg == 3 ? (k == 0 ? (odd ? k_cgp<true, true> : k_cgp<true, false>)
+                                     : (odd ? k_cgp<false, true> : k_cgp<false, false>))
+                  : deg == 1 ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
+                                       : (odd ? k_cgn<false, true> : k_cgn<false, false>))
+                             : (k == 0 ? (odd ? k_cg<true, false, true> : k_cg<true, false, false>)
+                                       : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);

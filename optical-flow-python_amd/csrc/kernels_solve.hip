@@ -86,6 +86,7 @@ struct PcgArgs {
   CgFlag *hflag;  // mapped host memory (may be null)
   double rtol;
   int maxiter;
+  float poly[4];  // k_cgp: M^-1 = (poly[0] + poly[1] B + poly[2] B^2 + poly[3] B^3) D^-1
 };
 
 // the shared prologue: returns 1 when the solve is finished (state written)
@@ -327,7 +328,8 @@ __global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands)
   const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
   const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
   const unsigned ps4 = (unsigned)(g.ps * 4);
-  const int lane = threadIdx.x, band = blockIdx.y * 4 + threadIdx.y;
+  // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
+  const int lane = threadIdx.x, band = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.y);
   const int jc = blockIdx.x * PCG_SW - 2 + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
   const bool out_lane = lane >= 1 && lane <= 62;
@@ -495,7 +497,8 @@ __global__ __launch_bounds__(256) void k_cgn(PcgArgs g, int k, int R, int nbands
   const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
   const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
   const unsigned ps4 = (unsigned)(g.ps * 4);
-  const int lane = threadIdx.x, band = blockIdx.y * 4 + threadIdx.y;
+  // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
+  const int lane = threadIdx.x, band = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.y);
   const int jc = blockIdx.x * PCG_SWN - 4 + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
   const bool out_lane = lane >= 2 && lane <= 61;
@@ -632,6 +635,329 @@ __global__ __launch_bounds__(256) void k_cgn(PcgArgs g, int k, int R, int nbands
           acc[4] += (double)cg_dot(rm, rm1);
         }
         YQ[u & 1] = yq;
+      }
+    }
+  }
+  write_partials<5>(acc, g.part, lds);
+}
+
+// ---------------------------------------------------------------------------
+// k_cgp: the fused, q-free CG iteration with a degree-3 polynomial
+// preconditioner in the 2x2 block-Jacobi splitting A = D - N, B = D^-1 N:
+//   M^-1 = (c0 + c1 B + c2 B^2 + c3 B^3) D^-1,
+// the Chebyshev polynomial that minimises max |1 - X p(X)| for the spectrum
+// of X = D^-1 A = I - B on [0.04, 2] (host: cheb_poly; 2 bounds the
+// spectrum because D + N is positive semidefinite).  p > 0 there, so M is
+// SPD.  Measured on Classic+NL stage-2 systems (RubberWhale, 1e-6 relative
+// residual): 0.54x the iterations of the first-order Neumann kernel k_cgn.
+//
+// z = M^-1 r by Horner, one neighbour exchange per stage:
+//   y = D^-1 r,  g2 = c2 y + c3 D^-1 N y,  g1 = c1 y + D^-1 N g2,
+//   z = c0 y + D^-1 N g1   (and r.z = c0 r.y + y.N g1).
+// The rho recurrence needs q.M^-1 q = sum_i c_i T_i with y_q = D^-1 q,
+// v1 = D^-1 N y_q:  T0 = y_q.q, T1 = y_q.N y_q, T2 = v1.N y_q (= v1.D v1),
+// T3 = v1.N v1 (each edge counted once, by its right / lower pixel).
+//
+// Pipeline (step n): A) r, y of row n-1; B) g2 of row n-2; C) g1 of row
+// n-3; D) z, p, x of row n-4; E) q, y_q of row n-5; F) v1 and the T terms
+// of row n-6.  Seven stencil stages deep, so a strip carries four halo
+// lanes per side (PCG_SWP = 112 output columns, lanes 4..59) and a band is
+// entered at row r0 - 7 and left at r1 + 5.
+// Arithmetic is on (u, v) pairs of one pixel (packed fp32: v_pk_fma_f32).
+// Each row's coefficients are staged once into a per-wave LDS ring (8 rows;
+// per pixel the (u, v) weight pairs of the edges right and below and D^-1
+// as (ia, ic), (ic, id); 32 KB per wave) that every stage reads; D itself
+// is re-formed from D^-1 where a stage needs it.  Vectors live in register
+// rings indexed by (row - (r0 - 7)); the loop is unrolled by eight so every
+// ring index is a compile-time constant.  Global loads run two steps ahead
+// (coefficients of row n+3, p_old of row n+2), r_in and x one step.
+#define PCG_SWP 112
+#define CG_ROW_OOB 0x40000000u
+
+struct CgRec {  // one LDS-ring row: pixel e of the lane, (u, v) pairs
+  cg_f2 wx[2], wy[2];  // weights of the edges right of / below the pixel
+  cg_f2 ma[2], mb[2];  // D^-1 columns: (ia, ic), (ic, id)
+};
+struct CgRaw {  // staged global loads of one coefficient row (plane order)
+  cg_f2 wxu, wyu, wxv, wyv, a, c, d;
+};
+
+__device__ __forceinline__ cg_f2 cg_lo(cg_f4 v) { return cg_f2{v.x, v.y}; }
+__device__ __forceinline__ cg_f2 cg_hi(cg_f4 v) { return cg_f2{v.z, v.w}; }
+__device__ __forceinline__ cg_f4 cg_cat(cg_f2 a, cg_f2 b) { return cg_f4{a.x, a.y, b.x, b.y}; }
+__device__ __forceinline__ cg_f2 cg_left2(cg_f2 v) { return cg_f2{cg_from_left(v.x), cg_from_left(v.y)}; }
+__device__ __forceinline__ cg_f2 cg_right2(cg_f2 v) { return cg_f2{cg_from_right(v.x), cg_from_right(v.y)}; }
+
+// N f of the middle row; wu = vertical weight pairs of the row above
+__device__ __forceinline__ cg_f4 cgr_nsum(cg_f4 up, cg_f4 mid, cg_f4 dn, const CgRec &c, const cg_f2 (&wu)[2]) {
+  const cg_f2 m0 = cg_lo(mid), m1 = cg_hi(mid);
+  const cg_f2 L = cg_left2(m1), Rt = cg_right2(m0), wl = cg_left2(c.wx[1]);
+  const cg_f2 s0 = wl * L + c.wx[0] * m1 + wu[0] * cg_lo(up) + c.wy[0] * cg_lo(dn);
+  const cg_f2 s1 = c.wx[0] * m0 + c.wx[1] * Rt + wu[1] * cg_hi(up) + c.wy[1] * cg_hi(dn);
+  return cg_cat(s0, s1);
+}
+__device__ __forceinline__ cg_f4 cgr_minv(const CgRec &m, cg_f4 r) {
+  const cg_f2 z0 = m.ma[0] * r.x + m.mb[0] * r.y;
+  const cg_f2 z1 = m.ma[1] * r.z + m.mb[1] * r.w;
+  return cg_cat(z0, z1);
+}
+// D f with D re-formed from the stored D^-1 (its 2x2 inverse; scalar-Jacobi
+// rows, ic = 0, give diag(1/ia, 1/id); all-zero records give D = 0)
+__device__ __forceinline__ cg_f4 cgr_diag(const CgRec &m, cg_f4 f) {
+  cg_f2 o[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float ia = m.ma[e].x, ic = m.ma[e].y, id = m.mb[e].y;
+    const float det = ia * id - ic * ic;
+    const float inv = det != 0.f ? __builtin_amdgcn_rcpf(det) : 0.f;
+    const cg_f2 da = cg_f2{id, -ic} * inv, db = cg_f2{-ic, ia} * inv;
+    const float fu = e ? f.z : f.x, fv = e ? f.w : f.y;
+    o[e] = da * fu + db * fv;
+  }
+  return cg_cat(o[0], o[1]);
+}
+
+template <bool FIRST, bool ODD>
+__global__ __launch_bounds__(256) void k_cgp(PcgArgs g, int k, int R, int nbands) {
+  __shared__ double lds[64];
+  __shared__ float4 ring[4][8][4][64];  // [wave][row slot][record quarter][lane]
+  const int H = g.H, W = g.W;
+  const unsigned rowb4 = (unsigned)g.P * 4u, rowb8 = (unsigned)g.P * 8u;
+  const size_t vbytes = (size_t)H * g.P * 8;
+  const __amdgpu_buffer_rsrc_t rc = cg_rsrc(g.coef, g.ps * 7 * 4);
+  const __amdgpu_buffer_rsrc_t rin = cg_rsrc(FIRST ? g.b : g.r_in, vbytes);
+  const __amdgpu_buffer_rsrc_t rpo = cg_rsrc(g.p_old, vbytes);
+  const __amdgpu_buffer_rsrc_t rx = cg_rsrc(g.x, vbytes);
+  const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
+  const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
+  const unsigned ps4 = (unsigned)(g.ps * 4);
+  // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
+  const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = blockIdx.y * 4 + wid;
+  const int jc = blockIdx.x * PCG_SWP - 8 + 2 * lane;
+  const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
+  const bool out_lane = lane >= 4 && lane <= 59;
+  const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
+  const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
+  const bool live = band < nbands;
+  const int r0 = band * R, r1 = min(r0 + R, H);
+  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
+  // row part of an offset: wave-uniform (SALU); rows outside [0, H) get
+  // CG_ROW_OOB, which keeps every lane's sum out of range without wrapping
+  // (lane parts are < 2^24 or CG_OOB; buffers < CG_ROW_OOB bytes, host-checked)
+  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb4 : CG_ROW_OOB); };
+  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb8 : CG_ROW_OOB); };
+  auto load_raw = [&](int t, CgRaw &c) {
+    const unsigned v = o4(t);
+    c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
+    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
+    c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
+    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
+    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
+    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
+    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
+  };
+  // raw row -> LDS ring slot (per pixel: wx, wy pairs; D^-1 columns)
+  auto put_rec = [&](int slot, const CgRaw &c) {
+    CgCoef cc;
+    cc.a = c.a;
+    cc.c = c.c;
+    cc.d = c.d;
+    const CgInv mi = cg_inv<true>(cc);
+    float4 *q = &ring[wid][slot][0][lane];
+    q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
+    q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
+    q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
+    q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
+  };
+  auto get_rec = [&](int slot) {
+    const float4 *q = &ring[wid][slot][0][lane];
+    const float4 a = q[0], b = q[64], c = q[128], d = q[192];
+    CgRec r;
+    r.wx[0] = cg_f2{a.x, a.y};
+    r.wy[0] = cg_f2{a.z, a.w};
+    r.wx[1] = cg_f2{b.x, b.y};
+    r.wy[1] = cg_f2{b.z, b.w};
+    r.ma[0] = cg_f2{c.x, c.y};
+    r.mb[0] = cg_f2{c.z, c.w};
+    r.ma[1] = cg_f2{d.x, d.y};
+    r.mb[1] = cg_f2{d.z, d.w};
+    return r;
+  };
+  auto get_wy = [&](int slot, cg_f2 (&wu)[2]) {  // vertical weight pairs only
+    const float2 *q = reinterpret_cast<const float2 *>(&ring[wid][slot][0][lane]);
+    const float2 a = q[1], b = q[129];
+    wu[0] = cg_f2{a.x, a.y};
+    wu[1] = cg_f2{b.x, b.y};
+  };
+  auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
+  auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
+  auto load_x = [&](int t) {
+    return (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
+  };
+  // dot products of output pixels only (select, not multiply: halo lanes
+  // may hold inf/nan)
+  const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;
+  auto mdot = [&](cg_f4 a, cg_f4 b) {
+    const cg_f2 p = cg_lo(a) * cg_lo(b), q = cg_hi(a) * cg_hi(b);
+    return (dm0 ? p.x + p.y : 0.f) + (dm1 ? q.x + q.y : 0.f);
+  };
+  const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const int ns = r0 - 7, ne = r1 + 5;
+
+  CgRaw SG[2];   // staged coefficient rows n+2, n+3
+  cg_f4 PO[8];   // p_old of rows n-4 .. n+2
+  cg_f4 RI[2];   // r_in of rows n-1, n
+  cg_f4 XI[2];   // x of rows n-4, n-3
+  if (live) {
+    // rows ns .. ns+2 (coefficients), ns, ns+1 (p_old), ns (r_in)
+    load_raw(ns, SG[0]);
+    PO[0] = load_po(ns);
+    PO[1] = load_po(ns + 1);
+    RI[0] = load_rin(ns);
+#pragma unroll
+    for (int s = 2; s < 8; ++s) PO[s] = zero4;
+    RI[1] = zero4;
+    XI[0] = XI[1] = zero4;
+  }
+  float alpha = 0.f, beta = 0.f;
+  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
+
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    {
+      // ring slot 0 <- row ns; slots 1..7 <- zero rows (read before written
+      // only by stages whose rows lie above the band's valid region)
+      put_rec(0, SG[0]);
+      CgRaw zr;
+      zr.wxu = zr.wyu = zr.wxv = zr.wyv = zr.a = zr.c = zr.d = cg_f2{0.f, 0.f};
+#pragma unroll
+      for (int s = 1; s < 8; ++s) put_rec(s, zr);
+      load_raw(ns + 1, SG[1]);
+      load_raw(ns + 2, SG[0]);
+    }
+    cg_f4 YR[4], G2[4], G1[4], PP[4], YQ[4], ZZ[2], V1[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) YR[s] = G2[s] = G1[s] = PP[s] = YQ[s] = zero4;
+    ZZ[0] = ZZ[1] = V1[0] = V1[1] = zero4;
+    for (int n0 = ns; n0 <= ne; n0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int n = n0 + u;
+        if (n > ne) break;
+        // ring slots: row n + d lives in PO / LDS slot (u + d) & 7, in the
+        // 4-rings at (u + d) & 3 and in the 2-rings at (u + d) & 1
+#define S8(d) ((u + (d) + 16) & 7)
+#define S4(d) ((u + (d) + 16) & 3)
+#define S2(d) ((u + (d) + 16) & 1)
+        // vertical weights of row n-7 (its slot is about to take row n+1)
+        cg_f2 wy7[2];
+        get_wy(S8(-7), wy7);
+        put_rec(S8(1), SG[S2(1)]);
+        load_raw(n + 3, SG[S2(1)]);
+        PO[S8(2)] = load_po(n + 2);
+        RI[S2(0)] = load_rin(n);
+        XI[S2(-3)] = load_x(n - 3);
+        // LDS records are read one stage ahead of their use (the ds_read
+        // latency overlaps the previous stage's arithmetic)
+        CgRec qn = get_rec(S8(-1));
+        cg_f2 wn[2];
+        get_wy(S8(-2), wn);
+        // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
+        {
+          const CgRec q1 = qn;
+          cg_f2 wu[2] = {wn[0], wn[1]};
+          qn = get_rec(S8(-2));
+          get_wy(S8(-3), wn);
+          cg_f4 r = RI[S2(-1)];
+          if (!FIRST) r -= alpha * (cgr_diag(q1, PO[S8(-1)]) - cgr_nsum(PO[S8(-2)], PO[S8(-1)], PO[S8(0)], q1, wu));
+          const cg_f4 y = cgr_minv(q1, r);
+          YR[S4(-1)] = y;
+          const int o = n - 1;
+          if (o >= r0 && o < r1) {
+            cg_st4(rro, soff8 + (unsigned)o * rowb8, r);
+            acc[4] += (double)mdot(r, r);
+            acc[3] += (double)(c0 * mdot(r, y));
+          }
+        }
+        // B) row n-2: g2 = c2 y + c3 D^-1 N y
+        {
+          const CgRec q2 = qn;
+          cg_f2 wu[2] = {wn[0], wn[1]};
+          qn = get_rec(S8(-3));
+          get_wy(S8(-4), wn);
+          const cg_f4 ny = cgr_nsum(YR[S4(-3)], YR[S4(-2)], YR[S4(-1)], q2, wu);
+          G2[S4(-2)] = c2 * YR[S4(-2)] + c3 * cgr_minv(q2, ny);
+        }
+        // C) row n-3: g1 = c1 y + D^-1 N g2
+        {
+          const CgRec q3 = qn;
+          cg_f2 wu[2] = {wn[0], wn[1]};
+          qn = get_rec(S8(-4));
+          get_wy(S8(-5), wn);
+          const cg_f4 ng = cgr_nsum(G2[S4(-4)], G2[S4(-3)], G2[S4(-2)], q3, wu);
+          G1[S4(-3)] = c1 * YR[S4(-3)] + cgr_minv(q3, ng);
+        }
+        // D) row n-4: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
+        {
+          const CgRec q4 = qn;
+          cg_f2 wu[2] = {wn[0], wn[1]};
+          qn = get_rec(S8(-5));
+          get_wy(S8(-6), wn);
+          const cg_f4 ng = cgr_nsum(G1[S4(-5)], G1[S4(-4)], G1[S4(-3)], q4, wu);
+          const cg_f4 yr = YR[S4(-4)];
+          const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
+          cg_f4 p = FIRST ? z : z + beta * PO[S8(-4)];
+          const int o = n - 4;
+          const bool rv = (unsigned)o < (unsigned)H;
+          if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
+          if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
+          PP[S4(-4)] = p;
+          ZZ[S2(-4)] = z;
+          if (o >= r0 && o < r1) {
+            const unsigned so = soff8 + (unsigned)o * rowb8;
+            cg_st4(rpn, so, p);
+            cg_st4(rx, so, FIRST ? zero4 : XI[S2(-4)] + alpha * PO[S8(-4)]);
+            acc[3] += (double)mdot(yr, ng);
+          }
+        }
+        // E) row n-5: q = A p, y_q = D^-1 q
+        {
+          const CgRec q5 = qn;
+          cg_f2 wu[2] = {wn[0], wn[1]};
+          qn = get_rec(S8(-6));
+          const cg_f4 pm = PP[S4(-5)];
+          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[S4(-6)], pm, PP[S4(-4)], q5, wu);
+          const cg_f4 yq = cgr_minv(q5, q);
+          YQ[S4(-5)] = yq;
+          const int o = n - 5;
+          if (o >= r0 && o < r1) {
+            acc[0] += (double)mdot(pm, q);
+            acc[1] += (double)mdot(q, ZZ[S2(-5)]);
+            acc[2] += (double)(c0 * mdot(q, yq));
+          }
+        }
+        // F) row n-6: N y_q, v1 = D^-1 N y_q, T1..T3
+        {
+          const CgRec q6 = qn;
+          const cg_f4 yq = YQ[S4(-6)];
+          const cg_f4 ny = cgr_nsum(YQ[S4(-7)], yq, YQ[S4(-5)], q6, wy7);
+          const cg_f4 v1 = cgr_minv(q6, ny);
+          const cg_f4 vu = V1[S2(-7)];
+          V1[S2(-6)] = v1;
+          const int o = n - 6;
+          if (o >= r0 && o < r1) {
+            // edges to the left and above, counted by this (right / lower)
+            // pixel: N v1 restricted to those edges
+            const cg_f2 v0 = cg_lo(v1), vv1 = cg_hi(v1);
+            const cg_f2 h0 = cg_left2(q6.wx[1]) * cg_left2(vv1) + wy7[0] * cg_lo(vu);
+            const cg_f2 h1 = q6.wx[0] * v0 + wy7[1] * cg_hi(vu);
+            const cg_f4 t = (c1 * yq + c2 * v1) * ny + (2.0f * c3) * v1 * cg_cat(h0, h1);
+            acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
+          }
+        }
+#undef S8
+#undef S4
+#undef S2
       }
     }
   }
