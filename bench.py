@@ -1,21 +1,23 @@
 """Benchmark: image pairs/s for Classic+NL-fast on 1920x1080 synthetic pairs
 (BASELINE.json metric; SURVEY.md §8d config 4, and config 5 across GPUs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--lanes L]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One process per GPU.  A step = every rank runs estimate_flow on its P
-device-resident pairs (inputs uploaded to HBM before timing: RGB -> gray/Lab,
-ROF, pyramids, GNC x levels x IRLS, all on the GPU) and, for N > 1, the flows
-are gathered to rank 0 with RCCL over xGMI.  Timed region: barrier +
-device sync on both sides, max over ranks.  value = pairs processed by all
-ranks / time (weak scaling: P pairs per GPU).
+device-resident pairs (default 8 = config 5's 64 pairs over 8 GPUs; inputs
+uploaded to HBM before timing: RGB -> gray/Lab, ROF, pyramids, GNC x levels
+x IRLS, all on the GPU), L of them in flight on concurrent streams
+(of_pairs_run), and, for N > 1, the flows are gathered to rank 0 with RCCL
+over xGMI.  Timed region: barrier + device sync on both sides, max over
+ranks.  value = pairs processed by all ranks / time (weak scaling: P pairs
+per GPU).
 
 Also reported (one JSON line on rank 0):
   roofline      dominant HBM kernel: algorithmic bytes per launch / mean
                 HIP-event duration of that kernel over a profiled replay of
-                the timed steps; peak 8 TB/s; traffic from profiles/ PMC if
-                present (else null)
+                one step with the pairs in sequence (lanes = 1); peak 8 TB/s;
+                traffic from profiles/ PMC if present (else null)
   cpu_baseline  the float64 C oracle (oracle/, OpenMP) on a bounded crop of
                 the same pair, scaled by pixel count to pairs/s
   ms_per_level  GPU time of each compute_flow_base (coarse -> fine, per stage)
@@ -56,7 +58,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pairs", type=int, default=1, help="pairs per GPU per step")
+    ap.add_argument("--pairs", type=int, default=8, help="pairs per GPU per step (config 5: 64 pairs / 8 GPUs)")
+    ap.add_argument("--lanes", type=int, default=3, help="concurrent pair pipelines per GPU (of_pairs_run)")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--method", default="classic+nl-fast")
@@ -108,11 +111,10 @@ def make_params(args):
     return P
 
 
-def run_step(ctx, P0, nslots, stats=None):
-    for s in range(nslots):
-        P = _abi.OfParams()
-        C.memmove(C.byref(P), C.byref(P0), C.sizeof(P0))  # alpha is updated per call
-        ctx.check(ctx.lib.of_pair_run(ctx.handle, s, C.byref(P), None if stats is None else C.byref(stats)))
+def run_step(ctx, P0, nslots, lanes):
+    """estimate_flow on device slots 0..nslots-1, `lanes` pairs in flight
+    (each lane its own HIP stream + host thread inside the library)."""
+    ctx.check(ctx.lib.of_pairs_run(ctx.handle, nslots, C.byref(P0), lanes, None))
 
 
 def cpu_baseline(args):
@@ -210,7 +212,7 @@ def main():
         ctx.check(lib.of_rccl_init(ctx.handle, obj[0], world, rank))
 
     def step():
-        run_step(ctx, P0, args.pairs)
+        run_step(ctx, P0, args.pairs, args.lanes)
         if world > 1:
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
 
@@ -241,11 +243,14 @@ def main():
     ktimes = {}
     pcg_levels = None
     if not args.no_profile:
-        # profiled replay of the timed steps: HIP events around every launch
-        # on the ctx stream (the stream the kernels run on)
+        # profiled replay of one step with the pairs run one after another
+        # (lanes = 1): HIP events around every launch on the stream the
+        # kernels run on, so a kernel's duration is not inflated by another
+        # pair's kernels sharing the CUs
+        rsteps = 1
         ctx.check(lib.of_set_profiling(ctx.handle, 2))  # keyed by kernel and level size
-        for _ in range(args.steps):
-            run_step(ctx, P0, args.pairs)
+        for _ in range(rsteps):
+            run_step(ctx, P0, args.pairs, 1)
         n = C.c_int(0)
         names = (C.c_char_p * 1024)()
         ms = (C.c_double * 1024)()
@@ -256,7 +261,7 @@ def main():
         per_level = {}
         for i in range(min(n.value, 1024)):
             name, lvl = names[i].decode().rsplit("@", 1)
-            rec = {"ms_total": ms[i] / args.steps, "launches": int(cnt[i]) / args.steps, "px": pxs[i] / args.steps}
+            rec = {"ms_total": ms[i] / rsteps, "launches": int(cnt[i]) / rsteps, "px": pxs[i] / rsteps}
             per_level[(name, int(lvl))] = rec
             agg = ktimes.setdefault(name, {"ms_total": 0.0, "launches": 0.0, "px": 0.0})
             for k in agg:
@@ -275,8 +280,10 @@ def main():
             "value": round(value, 4), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{args.method} on synth_pair({H},{W},seed) RGB, {args.pairs} pair(s)/GPU/step",
+            "config": {"workload": f"{args.method} on synth_pair({H},{W},seed) RGB, {args.pairs} pair(s)/GPU/step, "
+                                   f"{min(args.lanes, args.pairs)} in flight",
                        "method": args.method, "height": H, "width": W, "pairs_per_gpu": args.pairs,
+                       "lanes": min(args.lanes, args.pairs),
                        "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
                        "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -183,6 +183,12 @@ int of_compute_flow_base(of_ctx *ctx, of_params *params, const float *images, in
 int of_pair_upload(of_ctx *ctx, int slot, const float *im1, const float *im2, int H, int W, int C);
 /* run estimate_flow on device-resident slot; result stays on device */
 int of_pair_run(of_ctx *ctx, int slot, of_params *params, of_stats *stats);
+/* run estimate_flow on slots 0..nslots-1 with `lanes` concurrent pipelines
+ * (1..16; each its own HIP stream, device arena and solver state, driven by
+ * its own host thread; slot s runs on lane s % lanes).  params is copied per
+ * slot and not written back; stats (may be NULL) receives slot 0's.  Results
+ * are bitwise independent of `lanes`.  Returns when every slot is done. */
+int of_pairs_run(of_ctx *ctx, int nslots, const of_params *params, int lanes, of_stats *stats);
 /* D2H of a slot's flow (planar 2 x H x W) */
 int of_pair_download(of_ctx *ctx, int slot, float *out_uv);
 

@@ -19,7 +19,10 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels_img.hip"
@@ -123,6 +126,10 @@ struct of_ctx {
   std::map<int64_t, int> iter_hints;  // (H, W, solver) -> last iteration count
   double cur_px = 0;  // pixels processed by the launches being issued (profiling)
   std::vector<Slot> slots;
+  std::vector<of_ctx *> lanes;  // of_pairs_run pipelines: own stream, arena and solver state
+  std::mutex big_own;           // (parent) the big-phase token its lanes share
+  std::mutex *big = nullptr;    // (lane) token held through phases of >= big_px pixels
+  double big_px = 0;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
 };
@@ -887,6 +894,28 @@ void check_params(const of_params *P) {
           OF_ENOTSUP, "median_filter_size must be None, 3, 5 or 7");
 }
 
+// Lanes mode (of_pairs_run): a phase whose level has >= big_px pixels holds
+// the lanes' shared token until its GPU work has drained, so at most one pair
+// at a time streams a fine level's working set (1080p CG: ~190 MB, most of
+// the 256 MB Infinity Cache) while the other lanes run coarse levels, which
+// are latency-bound and need few bytes.  Outside lanes mode: no-op.
+struct BigPhase {
+  of_ctx *c;
+  bool held = false;
+  BigPhase(of_ctx *c_, double px) : c(c_) {
+    if (c->big && px >= c->big_px) {
+      c->big->lock();
+      held = true;
+    }
+  }
+  ~BigPhase() {
+    if (held) {
+      hipStreamSynchronize(c->stream);
+      c->big->unlock();
+    }
+  }
+};
+
 // compute_flow (hs.py:49-99, ba.py:57-138, classic_nl.py:89-198, alt_ba.py:81-187)
 // images: device 2nc planes; guide: device gc planes or p == nullptr;
 // uv_io: full-resolution flow (init in, result out).
@@ -897,6 +926,7 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
   hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
   HIPCHK(hipEventRecord(t0, c->stream));
   // preprocessing
+  std::unique_ptr<BigPhase> pre(new BigPhase(c, (double)H * W));
   Img img;
   if (P->texture) {
     const double alp = (P->method == OF_METHOD_HS || P->method == OF_METHOD_ALT_BA) ? 0.95 : P->alp;
@@ -930,6 +960,7 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
     cgpyr = build_pyramid(c, guide, P->gnc_pyramid_levels, P->gnc_pyramid_spacing);
   }
   HIPCHK(hipEventRecord(t1, c->stream));
+  pre.reset();
   F2 uv = uv_io, uvhat;
   if (P->method == OF_METHOD_ALT_BA) {
     uvhat = new_f2(c, H, W);
@@ -944,6 +975,7 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
     for (int l = nl - 1; l >= 0; --l) {
       const int h = lv[l].H, w = lv[l].W;
       hipEvent_t e0 = timing_event(c), e1 = timing_event(c);
+      BigPhase bp(c, (double)h * w);
       HIPCHK(hipEventRecord(e0, c->stream));
       if (uv.H != h || uv.W != w) {
         F2 nuv = new_f2(c, h, w);
@@ -1026,6 +1058,19 @@ void estimate_dev(of_ctx *c, of_params *P, const float *rgb1, const float *rgb2,
   }
 }
 
+// estimate_flow on a device-resident slot, on ctx c's stream (synchronous)
+void run_slot(of_ctx *c, const Slot &s, of_params *P, of_stats *st) {
+  if (st) memset(st, 0, sizeof(*st));
+  auto wall0 = std::chrono::steady_clock::now();
+  F2 uv = new_f2(c, s.H, s.W);
+  fill_f2(c, uv, 0.0f);
+  estimate_dev(c, P, s.rgb1, s.rgb2, s.H, s.W, s.C, uv, st);
+  f2_to_dense(c, uv, s.uv);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st)
+    st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+}
+
 int fail(of_ctx *c, const OfError &e) {
   if (c) c->err = e.msg;
   return e.code;
@@ -1099,6 +1144,8 @@ int of_ctx_create(int device, of_ctx **out) {
 
 int of_ctx_destroy(of_ctx *c) {
   if (!c) return OF_OK;
+  for (of_ctx *l : c->lanes) of_ctx_destroy(l);
+  c->lanes.clear();
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1255,16 +1302,82 @@ int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int 
 int of_pair_run(of_ctx *c, int slot, of_params *P, of_stats *st) {
   API_BEGIN(c)
   REQUIRE(slot >= 0 && slot < (int)c->slots.size() && c->slots[slot].rgb1, OF_EINVAL, "slot not uploaded");
-  Slot &s = c->slots[slot];
-  if (st) memset(st, 0, sizeof(*st));
-  auto wall0 = std::chrono::steady_clock::now();
-  F2 uv = new_f2(c, s.H, s.W);
-  fill_f2(c, uv, 0.0f);
-  estimate_dev(c, P, s.rgb1, s.rgb2, s.H, s.W, s.C, uv, st);
-  f2_to_dense(c, uv, s.uv);
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (st)
-    st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  run_slot(c, c->slots[slot], P, st);
+  API_END(c)
+}
+
+// Slots 0..nslots-1 on `lanes` concurrent pipelines.  Each lane is a child
+// context (own non-blocking stream, arena, CG state and host progress flag)
+// driven by its own host thread; slot s runs on lane s % lanes, so while one
+// pair is in a latency-bound phase (coarse levels, solver feed, host syncs)
+// another pair's kernels fill the CUs.  Every kernel is deterministic, so a
+// slot's flow does not depend on the lane count.  lanes == 1 runs the slots
+// in order on the ctx's own stream.
+int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats *st) {
+  API_BEGIN(c)
+  REQUIRE(P && nslots >= 1 && nslots <= (int)c->slots.size() && lanes >= 1 && lanes <= 16, OF_EINVAL,
+          "bad arguments");
+  for (int s = 0; s < nslots; ++s) REQUIRE(c->slots[s].rgb1 && c->slots[s].uv, OF_EINVAL, "slot not uploaded");
+  lanes = std::min(lanes, nslots);
+  if (lanes == 1) {
+    for (int s = 0; s < nslots; ++s) {
+      if (s) {
+        c->arena.reset();
+        c->tev_used = 0;
+      }
+      of_params Pc = *P;
+      run_slot(c, c->slots[s], &Pc, s == 0 ? st : nullptr);
+    }
+  } else {
+    while ((int)c->lanes.size() < lanes) {
+      of_ctx *l = nullptr;
+      const int rc = of_ctx_create(c->device, &l);
+      REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
+      c->lanes.push_back(l);
+    }
+    // big-phase token threshold in pixels, off by default (OF_BIG_PX=1048576
+    // measured 20.7 vs 21.8 pairs/s without it, 3 lanes at 1080p)
+    static const double big_px = getenv("OF_BIG_PX") ? atof(getenv("OF_BIG_PX")) : 0.0;
+    std::vector<std::thread> th;
+    std::vector<OfError> errs(lanes, OfError{OF_OK, ""});
+    for (int li = 0; li < lanes; ++li) {
+      of_ctx *l = c->lanes[li];
+      l->prof = c->prof;
+      l->big = big_px > 0 ? &c->big_own : nullptr;
+      l->big_px = big_px;
+      th.emplace_back([c, l, li, lanes, nslots, P, st, &errs] {
+        try {
+          HIPCHK(hipSetDevice(l->device));
+          for (int s = li; s < nslots; s += lanes) {
+            l->arena.reset();
+            l->tev_used = 0;
+            of_params Pc = *P;
+            run_slot(l, c->slots[s], &Pc, s == 0 ? st : nullptr);
+          }
+          flush_prof(l);
+        } catch (const OfError &e) {
+          errs[li] = e;
+          hipStreamSynchronize(l->stream);
+          l->pending.clear();
+          l->ev_used = 0;
+        } catch (const std::exception &e) {
+          errs[li] = OfError{OF_ENOMEM, e.what()};
+        }
+      });
+    }
+    for (auto &t : th) t.join();
+    for (int li = 0; li < lanes; ++li) {  // profiling: lane timings into the ctx's table
+      for (auto &kv : c->lanes[li]->ktimes) {
+        KTime &d = c->ktimes[kv.first];
+        d.ms += kv.second.ms;
+        d.px += kv.second.px;
+        d.n += kv.second.n;
+      }
+      c->lanes[li]->ktimes.clear();
+    }
+    for (auto &e : errs)
+      if (e.code != OF_OK) throw e;
+  }
   API_END(c)
 }
 

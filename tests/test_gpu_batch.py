@@ -49,6 +49,41 @@ def test_pair_slots_match_estimate_flow():
     ctx.close()
 
 
+def test_pairs_run_lanes_bitwise():
+    """of_pairs_run: the flow of every slot is bitwise the same whether the
+    slots run one after another (lanes=1), on 3 concurrent pipelines, or one
+    slot per of_pair_run call; argument errors raise ValueError."""
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    lib = ctx.lib
+    H, W = 72, 100
+    n = 5
+    for s in range(n):
+        a, b, _ = synth_pair(H, W, 20 + s)
+        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
+                                     H, W, 3))
+    P0 = _params("classic+nl-fast")
+
+    def flows():
+        out = np.empty((n, 2, H, W), np.float32)
+        for s in range(n):
+            ctx.check(lib.of_pair_download(ctx.handle, s, _native.ptr(out[s])))
+        return out
+
+    _run_slots(ctx, P0, n)
+    ref = flows()
+    assert np.all(np.isfinite(ref)) and np.abs(ref).max() > 0.1
+    for lanes in (1, 3, 8):
+        ctx.check(lib.of_pairs_run(ctx.handle, n, C.byref(P0), lanes, None))
+        np.testing.assert_array_equal(flows(), ref)
+    with pytest.raises(ValueError):
+        ctx.check(lib.of_pairs_run(ctx.handle, n + 1, C.byref(P0), 2, None))
+    with pytest.raises(ValueError):
+        ctx.check(lib.of_pairs_run(ctx.handle, n, C.byref(P0), 0, None))
+    ctx.close()
+
+
 def test_rccl_gather_single_rank():
     from optical_flow import _native
     from optical_flow.utils.synthetic import synth_pair
