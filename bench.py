@@ -49,7 +49,7 @@ KERNEL_BYTES_PER_PX = {
     "partial_deriv_hermite": 8 + 4 * 4 + 3 * 4 + 12,  # uv, I2/DX/DY/DXY, I1/I1x/I1y -> It/Ix/Iy
     "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ
     "wmf": 8 + 4 + 12 + 8,                 # uv, occ, Lab -> uv
-    "rof_iter": 4 + 8 + 8,                 # im, p -> p (per channel)
+    "rof_iters": 4 + 8 + 8,                # im, p -> p per channel, ROF_K iterations per launch
 }
 
 

@@ -258,8 +258,8 @@ void fill_f2(of_ctx *c, const F2 &f, float v) {
 void scale_img(of_ctx *c, const Img &m, float vlow, float vhigh, int mm_slot) {
   uint32_t *mm = c->d_mm + 2 * mm_slot;
   launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
-  Grid2 g = grid2(m.H, m.W);
-  launch(c, "minmax", k_minmax, g.grid, g.block, 0, (const float *)m.p, m.H, m.W, m.P, m.C, m.ps(), mm);
+  Grid2 gm = grid2(m.H, m.W, 256), g = grid2(m.H, m.W);
+  launch(c, "minmax", k_minmax, gm.grid, gm.block, 0, (const float *)m.p, m.H, m.W, m.P, m.C, m.ps(), mm);
   launch(c, "scale", k_scale, g.grid, g.block, 0, m.p, m.H, m.W, m.P, m.C, m.ps(), (const uint32_t *)mm, vlow, vhigh);
 }
 
@@ -339,9 +339,10 @@ Img rof_texture(of_ctx *c, const Img &in, double theta, int iters, double alp) {
   HIPCHK(hipMemsetAsync(p0, 0, sizeof(float2) * ps * in.C, c->stream));
   Grid2 g = grid2(in.H, in.W);
   const float th = (float)theta, delta = (float)(1.0 / (4.0 * theta));
-  for (int it = 0; it < iters; ++it) {
-    launch(c, "rof_iter", k_rof_iter, gz(g, in.C), g.block, 0, (const float *)nrm.p, (const float2 *)p0, p1, in.H,
-           in.W, nrm.P, ps, th, delta);
+  const dim3 rg((in.W + ROF_TW - 1) / ROF_TW, (in.H + ROF_TH - 1) / ROF_TH, in.C);  // 64 x 4 blocks
+  for (int it = 0; it < iters; it += ROF_K) {
+    launch(c, "rof_iters", k_rof_iters, rg, g.block, 0, (const float *)nrm.p, (const float2 *)p0, p1, in.H, in.W,
+           nrm.P, ps, th, delta, std::min(ROF_K, iters - it));
     std::swap(p0, p1);
   }
   Img out = new_img(c, in.H, in.W, in.C);
@@ -646,8 +647,11 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       return ak;
     };
     if (deg == 3) {
+      // Chebyshev interval of the block-Jacobi-scaled spectrum; OF_CG_CHEB_A
+      // overrides the lower end (A/B measurements)
+      static const double cheb_a = getenv("OF_CG_CHEB_A") ? atof(getenv("OF_CG_CHEB_A")) : 0.04;
       double cb[4];
-      cheb_poly(3, 0.04, 2.0, cb);
+      cheb_poly(3, cheb_a, 2.0, cb);
       for (int i = 0; i < 4; ++i) a.poly[i] = (float)cb[i];
     }
     a.hflag = c->d_flag;
@@ -1042,7 +1046,7 @@ void estimate_dev(of_ctx *c, of_params *P, const float *rgb1, const float *rgb2,
   launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
   if (C == 3) {
     const long n = (long)H * W * 3;
-    launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<long>((n + 255) / 256, 1024)), dim3(256), 0, rgb1, n, mm);
+    launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<long>((n + 255) / 256, 256)), dim3(256), 0, rgb1, n, mm);
   }
   Grid2 g = grid2(H, W);
   launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, rgb1, rgb2, H, W, C, gray.p, gray.P, gray.ps(),
@@ -1460,7 +1464,7 @@ int of_preprocess(of_ctx *c, const float *rgb1, const float *rgb2, int H, int W,
   Img gray = new_img(c, H, W, 2), g3 = new_img(c, H, W, 3);
   uint32_t *mm = c->d_mm + 2 * 8;
   launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
-  launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0,
+  launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<size_t>((n + 255) / 256, 256)), dim3(256), 0,
          (const float *)d1, (long)n, mm);
   Grid2 g = grid2(H, W);
   launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, (const float *)d1, (const float *)d2, H, W, 3, gray.p, gray.P,

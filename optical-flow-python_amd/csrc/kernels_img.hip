@@ -27,7 +27,19 @@ __global__ void k_minmax(const float *__restrict__ a, int H, int W, int P, int p
     lo = min(lo, (uint32_t)__shfl_down((int)lo, off, 64));
     hi = max(hi, (uint32_t)__shfl_down((int)hi, off, 64));
   }
-  if (((threadIdx.x + threadIdx.y * blockDim.x) & 63) == 0) {
+  // one atomic pair per block (launched with <= 256 blocks): thousands of
+  // same-address atomics from every wave serialise at the memory side
+  __shared__ uint32_t s_lo[OF_BY], s_hi[OF_BY];
+  if (threadIdx.x == 0) {
+    s_lo[threadIdx.y] = lo;
+    s_hi[threadIdx.y] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    for (int w = 1; w < OF_BY; ++w) {
+      lo = min(lo, s_lo[w]);
+      hi = max(hi, s_hi[w]);
+    }
     atomicMin(&mm[0], lo);
     atomicMax(&mm[1], hi);
   }
@@ -53,7 +65,10 @@ __global__ void k_rgb_max(const float *__restrict__ rgb, long n, uint32_t *mm) {
   for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x)
     hi = max(hi, f2ord(rgb[k]));
   for (int off = 32; off > 0; off >>= 1) hi = max(hi, (uint32_t)__shfl_down((int)hi, off, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(&mm[1], hi);
+  __shared__ uint32_t s_hi[4];  // 256-thread blocks: one atomic per block
+  if ((threadIdx.x & 63) == 0) s_hi[threadIdx.x >> 6] = hi;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&mm[1], max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3])));
 }
 
 __device__ __forceinline__ float q_u8(float x) {
@@ -104,21 +119,85 @@ __device__ __forceinline__ float rof_div(const float2 *__restrict__ p, int i, in
   return d;
 }
 
-__global__ void k_rof_iter(const float *__restrict__ im, const float2 *__restrict__ pin, float2 *__restrict__ pout,
-                           int H, int W, int P, size_t ps, float theta, float delta) {
+// ROF_K primal-dual iterations per launch (temporal blocking).  A block of
+// 4 waves owns a ROF_TW x ROF_TH tile of one channel plus a ROF_K-wide halo:
+// lane = column (ROF_RW = 64 = ROF_TW + 2 ROF_K), wave w = ROF_RPW
+// consecutive rows, held in registers.  One iteration of a pixel's p reads
+// p only at Chebyshev distance <= 1, so after `iters` <= ROF_K iterations the
+// tile is exact; HBM traffic is one read of im + p and one write of p per
+// launch instead of per iteration.  Horizontal neighbours are DPP lane
+// shifts, vertical ones registers; only the rows at a wave boundary go
+// through LDS (two barriers per iteration).  Per iteration:
+//   u = im + theta div p   (div: backward differences, term dropped at
+//                           image column / row 0)
+//   p <- (p + delta grad u) / max(1, |.|)   (grad 0 at the last column / row)
+// (image_processing.py:104-127).  Pixels outside the image hold p = im = 0
+// and are never read by pixels inside it.  1 / max(1, |.|) is an rsq.
+#define ROF_RW 64
+#define ROF_K 8
+#define ROF_TW (ROF_RW - 2 * ROF_K)
+#define ROF_RPW 32
+#define ROF_TH (4 * ROF_RPW - 2 * ROF_K)
+__device__ __forceinline__ float rof_from_left(float v) {  // lane l <- lane l-1, lane 0 <- 0
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float rof_from_right(float v) {  // lane l <- lane l+1, lane 63 <- 0
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+__global__ __launch_bounds__(256) void k_rof_iters(const float *__restrict__ im, const float2 *__restrict__ pin,
+                                                   float2 *__restrict__ pout, int H, int W, int P, size_t ps,
+                                                   float theta, float delta, int iters) {
+  __shared__ float s_py[4][64], s_u[4][64];  // wave-boundary rows: p_y of the last, u of the first
   im += blockIdx.z * ps;
   pin += blockIdx.z * ps;
   pout += blockIdx.z * ps;
-  OF_FOR_PIXELS(H, W) {
-    if (j >= W) continue;
-    size_t k = (size_t)i * P + j;
-    float u = im[k] + theta * rof_div(pin, i, j, P);
-    float gx = j < W - 1 ? im[k + 1] + theta * rof_div(pin, i, j + 1, P) - u : 0.0f;
-    float gy = i < H - 1 ? im[k + P] + theta * rof_div(pin, i + 1, j, P) - u : 0.0f;
-    float2 q = pin[k];
-    float a = q.x + delta * gx, b = q.y + delta * gy;
-    float nrm = fmaxf(sqrtf(a * a + b * b), 1.0f);
-    pout[k] = make_float2(a / nrm, b / nrm);
+  const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
+  const int gj = blockIdx.x * ROF_TW - ROF_K + lane;
+  const int gr0 = blockIdx.y * ROF_TH - ROF_K + w * ROF_RPW;  // image row of the wave's first row
+  const bool colin = (unsigned)gj < (unsigned)W, left = gj > 0, right = gj < W - 1;
+  float I[ROF_RPW], U[ROF_RPW];
+  float2 Q[ROF_RPW];
+#pragma unroll
+  for (int r = 0; r < ROF_RPW; ++r) {
+    const int gi = gr0 + r;
+    const bool in = colin && (unsigned)gi < (unsigned)H;
+    const size_t k = (size_t)gi * P + gj;
+    I[r] = in ? im[k] : 0.0f;
+    Q[r] = in ? pin[k] : make_float2(0.0f, 0.0f);
+  }
+  for (int it = 0; it < iters; ++it) {
+    s_py[w][lane] = Q[ROF_RPW - 1].y;
+    __syncthreads();
+    float pya = w > 0 ? s_py[w - 1][lane] : 0.0f;  // p_y of the row above the wave's first row
+#pragma unroll
+    for (int r = 0; r < ROF_RPW; ++r) {
+      const float2 q = Q[r];
+      const float pl = rof_from_left(q.x);
+      float d = left ? q.x - pl : q.x;
+      d += gr0 + r > 0 ? q.y - pya : q.y;
+      U[r] = I[r] + theta * d;
+      pya = q.y;
+    }
+    s_u[w][lane] = U[0];
+    __syncthreads();
+    const float ub = w < 3 ? s_u[w + 1][lane] : 0.0f;  // u of the row below the wave's last row
+#pragma unroll
+    for (int r = 0; r < ROF_RPW; ++r) {
+      const float u = U[r], ur = rof_from_right(u), ud = r + 1 < ROF_RPW ? U[r + 1] : ub;
+      const float gx = right ? ur - u : 0.0f;
+      const float gy = gr0 + r < H - 1 ? ud - u : 0.0f;
+      const float a = Q[r].x + delta * gx, b = Q[r].y + delta * gy;
+      const float s2 = a * a + b * b;
+      const float inv = s2 > 1.0f ? __builtin_amdgcn_rsqf(s2) : 1.0f;
+      Q[r] = make_float2(a * inv, b * inv);
+    }
+  }
+  if (lane >= ROF_K && lane < ROF_K + ROF_TW && colin) {
+#pragma unroll
+    for (int r = 0; r < ROF_RPW; ++r) {
+      const int gi = gr0 + r, tr = w * ROF_RPW + r;  // row inside the block's region
+      if (tr >= ROF_K && tr < ROF_K + ROF_TH && gi < H) pout[(size_t)gi * P + gj] = Q[r];
+    }
   }
 }
 

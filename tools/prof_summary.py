@@ -108,10 +108,10 @@ def main():
         if hk and mk and sum(hk) + sum(mk) > 0:
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
         key = {"k_pcg_iter<true>": "pcg_iter", "k_pcg_iter<false>": "pcg_iter",
-               "k_flow_operator": "flow_operator", "k_wmf<3, 8>": "wmf", "k_rof_iter": "rof_iter",
+               "k_flow_operator": "flow_operator", "k_wmf<3, 8>": "wmf", "k_rof_iters": "rof_iters",
                "k_update_occ": "update_occ", "k_partial_deriv<1>": "partial_deriv_hermite"}.get(n)
         if key in bench.KERNEL_BYTES_PER_PX:
-            px = a.H * a.W * (2 if key == "rof_iter" else 1)
+            px = a.H * a.W * (2 if key == "rof_iters" else 1)
             alg = bench.KERNEL_BYTES_PER_PX[key] * px
             rec["alg_MB"] = round(alg / 1e6, 3)
             rec["alg_GBps"] = round(alg / (mean_us * 1e-6) / 1e9, 1)
