@@ -105,6 +105,8 @@ struct Slot {
 
 }  // namespace
 
+#define OF_SOLVE_RING 256
+
 struct of_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -112,7 +114,19 @@ struct of_ctx {
   Arena arena;
   PcgState *d_state = nullptr, *h_state = nullptr;  // h_state: 2 pinned slots
   hipEvent_t ev_state[2] = {nullptr, nullptr};
-  CgFlag *h_flag = nullptr, *d_flag = nullptr;  // mapped coherent host memory
+  // CG solves: per-solve progress flags (mapped coherent host memory) and
+  // copies of the final state (pinned), a ring of OF_SOLVE_RING; a solve's
+  // statistics are read at the next stream synchronisation, so a CG solve
+  // does not end in one
+  CgFlag *h_flag = nullptr, *d_flag = nullptr;
+  PcgState *h_ring = nullptr;
+  int ring_next = 0;
+  struct PendingSolve {
+    int slot;
+    double px;
+    of_stats *st;
+  };
+  std::vector<PendingSolve> pend;
   double *d_partials = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
@@ -458,6 +472,8 @@ struct SolveResult {
   int iters;
   int done;
   double rel;
+  int slot = -1;  // >= 0: CG solve whose state is still in flight (h_ring[slot])
+  double px = 0;
 };
 
 // grid for the 2-pixels-per-thread solver kernels, <= PCG_MAX_BLOCKS blocks
@@ -501,8 +517,7 @@ int run_chunked(of_ctx *c, int maxiter, int first, int max_chunk, Enq enqueue_it
 // mapped host flag; stop enqueueing as soon as a prologue has declared the
 // solve done.  Returns the number of launches enqueued.
 template <typename Enq>
-int run_fed(of_ctx *c, int nmax, int depth, Enq enqueue_iter) {
-  volatile CgFlag *f = c->h_flag;
+int run_fed(of_ctx *c, volatile CgFlag *f, int nmax, int depth, Enq enqueue_iter) {
   f->done = 0;
   f->iter = 0;
   f->k = -1;
@@ -528,6 +543,8 @@ int run_fed(of_ctx *c, int nmax, int depth, Enq enqueue_iter) {
   }
   return enq;
 }
+
+void drain_solves(of_ctx *c);
 
 // iteration-count hint of the last solve with this size and solver
 int& iter_hint(of_ctx *c, int H, int W, int solver) {
@@ -654,8 +671,16 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       cheb_poly(3, cheb_a, 2.0, cb);
       for (int i = 0; i < 4; ++i) a.poly[i] = (float)cb[i];
     }
-    a.hflag = c->d_flag;
-    const int enq = run_fed(c, a.maxiter + 1, 3, [&](int k) {
+    // ring slot of this solve; a slot is reused only after a synchronisation
+    // has drained its previous solve
+    if ((int)c->pend.size() >= OF_SOLVE_RING - 1) {
+      HIPCHK(hipStreamSynchronize(c->stream));
+      drain_solves(c);
+    }
+    const int slot = c->ring_next;
+    c->ring_next = (slot + 1) % OF_SOLVE_RING;
+    a.hflag = c->d_flag + slot;
+    const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
       auto kern = deg == 3 ? (k == 0 ? (odd ? k_cgp<true, true> : k_cgp<true, false>)
                                      : (odd ? k_cgp<false, true> : k_cgp<false, false>))
@@ -666,11 +691,11 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
-    HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const PcgState &s = c->h_state[0];
-    note_active(c, "pcg_iter", s.iter + 1, (double)H * W);
-    return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
+    HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    SolveResult r{0, 0, 0.0};
+    r.slot = slot;
+    r.px = (double)H * W;
+    return r;
   }
   // red-black block SOR
   Grid2 g = grid2(H, W, PCG_MAX_BLOCKS);
@@ -702,12 +727,34 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
   return {s.iter, s.done, 0.0};
 }
 
-void note_solve(of_stats *st, const SolveResult &r) {
+void note_solve_now(of_stats *st, const SolveResult &r) {
   if (!st) return;
   st->solves++;
   st->solver_iters_total += r.iters;
   st->solver_iters_max = std::max(st->solver_iters_max, r.iters);
   if (r.done == 2) st->solves_not_converged++;
+}
+
+// the final state of a deferred CG solve (valid after a stream sync)
+SolveResult resolved(of_ctx *c, int slot) {
+  const PcgState &s = c->h_ring[slot];
+  return {s.iter, s.done, s.bnorm > 0 ? std::sqrt(s.rr) / s.bnorm : 0.0};
+}
+
+// statistics of the CG solves since the last stream synchronisation (call
+// only after one)
+void drain_solves(of_ctx *c) {
+  for (const auto &p : c->pend) {
+    const SolveResult r = resolved(c, p.slot);
+    note_solve_now(p.st, r);
+    note_active(c, "pcg_iter", r.iters + 1, p.px);
+  }
+  c->pend.clear();
+}
+
+void note_solve(of_ctx *c, of_stats *st, const SolveResult &r) {
+  if (r.slot >= 0) c->pend.push_back({r.slot, r.px, st});
+  else note_solve_now(st, r);
 }
 
 double norm2(of_ctx *c, const F2 &x) {
@@ -717,6 +764,7 @@ double norm2(of_ctx *c, const F2 &x) {
          c->d_norm);
   HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  drain_solves(c);
   return *c->h_norm;
 }
 
@@ -779,7 +827,7 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
   for (int it = 0; it < P->max_warping_iters; ++it) {
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
-    note_solve(st, solve(c, P, coef, rhs, x));
+    note_solve(c, st, solve(c, P, coef, rhs, x));
     c->cur_px = (double)H * W;
     if (std::sqrt(norm2(c, x)) < 1e-3) break;
     launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)x.p, P->limit_update, H, W, uv.P);
@@ -811,7 +859,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     for (int jl = 0; jl < max_linear; ++jl) {
       flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
-      note_solve(st, solve(c, P, coef, rhs, x));
+      note_solve(c, st, solve(c, P, coef, rhs, x));
       c->cur_px = (double)H * W;
       const bool filt = P->median_filter_size != 0;
       launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
@@ -855,7 +903,7 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
     bool have_duv = false;
     for (int jl = 0; jl < P->max_linear; ++jl) {
       flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
-      note_solve(st, solve(c, P, coef, rhs, x));
+      note_solve(c, st, solve(c, P, coef, rhs, x));
       c->cur_px = (double)H * W;
       // duv = clip(x): computed as (0 + clip(x))
       HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
@@ -1021,6 +1069,7 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
   if (res.H == H && res.W == W && res.p != uv_io.p)
     HIPCHK(hipMemcpyAsync(uv_io.p, res.p, sizeof(float2) * (size_t)H * uv_io.P, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  drain_solves(c);
   if (st) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, t0, t1));
@@ -1091,11 +1140,16 @@ thread_local std::string g_err;
     ctx->arena.reset();            \
     ctx->tev_used = 0;
 #define API_END(ctx)                         \
+  if (!ctx->pend.empty()) {                  \
+    HIPCHK(hipStreamSynchronize(ctx->stream)); \
+    drain_solves(ctx);                       \
+  }                                          \
   flush_prof(ctx);                           \
   return OF_OK;                              \
   }                                          \
   catch (const OfError &e) {                 \
     ctx->pending.clear();                    \
+    ctx->pend.clear();                       \
     ctx->ev_used = 0;                        \
     return fail(ctx, e);                     \
   }                                          \
@@ -1129,7 +1183,8 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_state, sizeof(PcgState)));
     HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&c->h_flag, sizeof(CgFlag), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc(&c->h_flag, OF_SOLVE_RING * sizeof(CgFlag), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc(&c->h_ring, OF_SOLVE_RING * sizeof(PcgState), hipHostMallocDefault));
     HIPCHK(hipHostGetDevicePointer((void **)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
@@ -1166,6 +1221,7 @@ int of_ctx_destroy(of_ctx *c) {
   hipFree(c->d_state);
   hipHostFree(c->h_state);
   if (c->h_flag) hipHostFree(c->h_flag);
+  if (c->h_ring) hipHostFree(c->h_ring);
   hipFree(c->d_partials);
   hipFree(c->d_mm);
   hipFree(c->d_norm);
@@ -1333,19 +1389,24 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       run_slot(c, c->slots[s], &Pc, s == 0 ? st : nullptr);
     }
   } else {
-    while ((int)c->lanes.size() < lanes) {
+    // lane 0 is the ctx itself (its stream), lanes 1.. are child contexts:
+    // `lanes` streams in all, within GPU_MAX_HW_QUEUES (4) for lanes <= 4
+    while ((int)c->lanes.size() < lanes - 1) {
       of_ctx *l = nullptr;
       const int rc = of_ctx_create(c->device, &l);
       REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
       c->lanes.push_back(l);
+
     }
-    // big-phase token threshold in pixels, off by default (OF_BIG_PX=1048576
-    // measured 20.7 vs 21.8 pairs/s without it, 3 lanes at 1080p)
-    static const double big_px = getenv("OF_BIG_PX") ? atof(getenv("OF_BIG_PX")) : 0.0;
+    // big-phase token threshold in pixels (OF_BIG_PX overrides; 0 = off).
+    // 8 1080p pairs, 2 lanes: 22.5 pairs/s with the token in three runs
+    // (16-18 without; 20.5 with one lane) -- two lanes' fine-level CG
+    // kernels, one 128-KB-LDS block per CU each, otherwise stall each other
+    static const double big_px = getenv("OF_BIG_PX") ? atof(getenv("OF_BIG_PX")) : (double)(1 << 20);
     std::vector<std::thread> th;
     std::vector<OfError> errs(lanes, OfError{OF_OK, ""});
     for (int li = 0; li < lanes; ++li) {
-      of_ctx *l = c->lanes[li];
+      of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
       l->big = big_px > 0 ? &c->big_own : nullptr;
       l->big_px = big_px;
@@ -1358,7 +1419,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
             of_params Pc = *P;
             run_slot(l, c->slots[s], &Pc, s == 0 ? st : nullptr);
           }
-          flush_prof(l);
+          if (l != c) flush_prof(l);
         } catch (const OfError &e) {
           errs[li] = e;
           hipStreamSynchronize(l->stream);
@@ -1370,14 +1431,15 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       });
     }
     for (auto &t : th) t.join();
-    for (int li = 0; li < lanes; ++li) {  // profiling: lane timings into the ctx's table
-      for (auto &kv : c->lanes[li]->ktimes) {
+    c->big = nullptr;
+    for (int li = 1; li < lanes; ++li) {  // profiling: lane timings into the ctx's table
+      for (auto &kv : c->lanes[li - 1]->ktimes) {
         KTime &d = c->ktimes[kv.first];
         d.ms += kv.second.ms;
         d.px += kv.second.px;
         d.n += kv.second.n;
       }
-      c->lanes[li]->ktimes.clear();
+      c->lanes[li - 1]->ktimes.clear();
     }
     for (auto &e : errs)
       if (e.code != OF_OK) throw e;
@@ -1565,6 +1627,10 @@ int of_solve(of_ctx *c, const of_params *P, const float *coef, const float *rhs,
   SolveResult r = solve(c, P, cf, b, xx);
   download_f2(c, xx, x);
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (r.slot >= 0) {
+    note_active(c, "pcg_iter", resolved(c, r.slot).iters + 1, r.px);
+    r = resolved(c, r.slot);
+  }
   if (iters) *iters = r.iters;
   if (rel_residual) *rel_residual = r.rel;
   API_END(c)
