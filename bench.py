@@ -16,8 +16,8 @@ per GPU).
 Also reported (one JSON line on rank 0):
   roofline      dominant HBM kernel: algorithmic bytes per launch / mean
                 HIP-event duration of that kernel over a profiled replay of
-                one step with the pairs in sequence (lanes = 1); peak 8 TB/s;
-                traffic from profiles/ PMC if present (else null)
+                one timed step (same pairs and lanes); peak 8 TB/s; traffic
+                from profiles/ PMC if present (else null)
   cpu_baseline  the float64 C oracle (oracle/, OpenMP) on a bounded crop of
                 the same pair, scaled by pixel count to pairs/s
   ms_per_level  GPU time of each compute_flow_base (coarse -> fine, per stage)
@@ -166,24 +166,26 @@ def roofline_of(ktimes, per_level):
     act = dom + ".active"
 
     def fig(rec, arec):
+        """achieved = algorithmic bytes of the launches that did work / time
+        of all launches; mean_launch_ms = time / all launches (what the
+        rocprofv3 --stats average of the kernel measures)"""
         work = arec if arec and arec["launches"] else rec
-        px_per_launch = work["px"] / work["launches"]
-        avg_ms = rec["ms_total"] / work["launches"]
-        ach = KERNEL_BYTES_PER_PX[dom] * px_per_launch / (avg_ms * 1e-3) / 1e9
-        return round(ach, 1), round(avg_ms, 5), int(px_per_launch), work["launches"]
+        ach = KERNEL_BYTES_PER_PX[dom] * work["px"] / (rec["ms_total"] * 1e-3) / 1e9
+        return (round(ach, 1), round(rec["ms_total"] / rec["launches"], 5), int(work["px"] / work["launches"]),
+                work["launches"], round(rec["ms_total"] / work["launches"], 5))
 
-    ach, avg_ms, ppl, nact = fig(hbm[dom], ktimes.get(act))
+    ach, avg_ms, ppl, nact, act_ms = fig(hbm[dom], ktimes.get(act))
     out = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, "all"),
-           "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": avg_ms, "px_per_launch": ppl,
-           "launches_per_step": hbm[dom]["launches"], "active_launches_per_step": nact}
+           "bytes_per_px": KERNEL_BYTES_PER_PX[dom], "mean_launch_ms": avg_ms, "mean_active_launch_ms": act_ms,
+           "px_per_active_launch": ppl, "launches_per_step": hbm[dom]["launches"], "active_launches_per_step": nact}
     lv = [(px, rec) for (n, px), rec in per_level.items() if n == dom]
     if lv:
         px, rec = max(lv, key=lambda t: t[0])
-        a2, m2, p2, n2 = fig(rec, per_level.get((act, px)))
+        a2, m2, p2, n2, am2 = fig(rec, per_level.get((act, px)))
         out["finest"] = {"px_per_launch": p2, "achieved": a2, "frac": round(a2 / HBM_PEAK_GBS, 4),
-                         "mean_launch_ms": m2, "launches_per_step": rec["launches"], "active_launches_per_step": n2,
-                         "traffic": load_pmc_traffic(dom, "finest")}
+                         "mean_launch_ms": m2, "mean_active_launch_ms": am2, "launches_per_step": rec["launches"],
+                         "active_launches_per_step": n2, "traffic": load_pmc_traffic(dom, "finest")}
     return out
 
 
@@ -243,14 +245,12 @@ def main():
     ktimes = {}
     pcg_levels = None
     if not args.no_profile:
-        # profiled replay of one step with the pairs run one after another
-        # (lanes = 1): HIP events around every launch on the stream the
-        # kernels run on, so a kernel's duration is not inflated by another
-        # pair's kernels sharing the CUs
+        # profiled replay of one step, same pairs and lanes as the timed
+        # steps: HIP events around every launch on the stream it runs on
         rsteps = 1
         ctx.check(lib.of_set_profiling(ctx.handle, 2))  # keyed by kernel and level size
         for _ in range(rsteps):
-            run_step(ctx, P0, args.pairs, 1)
+            run_step(ctx, P0, args.pairs, args.lanes)
         n = C.c_int(0)
         names = (C.c_char_p * 1024)()
         ms = (C.c_double * 1024)()

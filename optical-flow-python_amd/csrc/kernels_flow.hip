@@ -404,6 +404,18 @@ struct WmfRec<1> {
 
 typedef float wmf_v2f __attribute__((ext_vector_type(2)));
 
+// weight of region sample s for a pixel of guide colour (c01, c2):
+// max(2^(nk |dlab|^2) occ, 1e-10), channels 0-1 in packed fp32
+__device__ __forceinline__ float wmf_w(const float4 &s, wmf_v2f c01, float c2, float nk) {
+  const wmf_v2f e = wmf_v2f{s.x, s.y} - c01, q = e * e;
+  const float e2 = s.z - c2;
+  return fmaxf(__builtin_amdgcn_exp2f(fmaf(e2, e2, q.x + q.y) * nk) * s.w, 1e-10f);
+}
+__device__ __forceinline__ float wmf_w(const float2 &s, wmf_v2f c01, float, float nk) {
+  const float e = s.x - c01.x;
+  return fmaxf(__builtin_amdgcn_exp2f(e * e * nk) * s.y, 1e-10f);
+}
+
 template <int NPER>
 __device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
   constexpr int N = NPER * 64;
@@ -490,14 +502,12 @@ __global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const
 #pragma unroll
     for (int c = 0; c < GC; ++c) cg[c] = cf[c];
   }
+  const wmf_v2f c01 = {cg[0], cg[1]};
   // total weight of the lane's window (row-major window order)
   double tot = 0.0;
   for (int dy = 0; dy <= 2 * hsz; ++dy) {
     const T *row = smp + (py + dy) * RW + px;
-    for (int dx = 0; dx <= 2 * hsz; ++dx) {
-      const T s = row[dx];
-      tot += (double)fmaxf(__builtin_amdgcn_exp2f(R::d2(s, cg) * nk) * R::occ(s), 1e-10f);
-    }
+    for (int dx = 0; dx <= 2 * hsz; ++dx) tot += (double)wmf_w(row[dx], c01, cg[2], nk);
   }
   const double half = 0.5 * tot;
   const unsigned span = 2u * hsz;
@@ -505,39 +515,30 @@ __global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const
   unsigned resu = 0, resv = 0;
   bool du = !live, dv = !live;
   for (int k0 = 0; k0 < N; k0 += 8) {
+    // keys are wave-uniform: each sample record is one broadcast LDS read,
+    // the per-lane part is the window test
     unsigned ka[8], kb[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       ka[i] = ku[k0 + i];
       kb[i] = kv[k0 + i];
     }
-    wmf_v2f w[8];
+    float wa[8], wb[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu, ryb = kb[i] >> 8, rxb = kb[i] & 0xffu;
       const bool ina = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
       const bool inb = (ryb - (unsigned)py) <= span && (rxb - (unsigned)px) <= span;
-      const T sa = smp[ina ? rya * RW + rxa : 0];
-      const T sb = smp[inb ? ryb * RW + rxb : 0];
-      const float *fa = reinterpret_cast<const float *>(&sa);
-      const float *fb = reinterpret_cast<const float *>(&sb);
-      wmf_v2f d2 = {0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < GC; ++c) {
-        const wmf_v2f e = wmf_v2f{fa[c], fb[c]} - cg[c];
-        d2 += e * e;
-      }
-      d2 *= nk;
-      wmf_v2f ww = {__builtin_amdgcn_exp2f(d2.x), __builtin_amdgcn_exp2f(d2.y)};
-      ww *= wmf_v2f{R::occ(sa), R::occ(sb)};
-      ww.x = ina ? fmaxf(ww.x, 1e-10f) : 0.0f;
-      ww.y = inb ? fmaxf(ww.y, 1e-10f) : 0.0f;
-      w[i] = ww;
+      // padding keys (0xffff) are outside every window; read any record
+      const float xa = wmf_w(smp[ka[i] == 0xffffu ? 0u : rya * RW + rxa], c01, cg[2], nk);
+      const float xb = wmf_w(smp[kb[i] == 0xffffu ? 0u : ryb * RW + rxb], c01, cg[2], nk);
+      wa[i] = ina ? xa : 0.0f;
+      wb[i] = inb ? xb : 0.0f;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      cu += (double)w[i].x;
-      cv += (double)w[i].y;
+      cu += (double)wa[i];
+      cv += (double)wb[i];
       const bool xa = !du && cu >= half, xb = !dv && cv >= half;
       resu = xa ? ka[i] : resu;
       resv = xb ? kb[i] : resv;

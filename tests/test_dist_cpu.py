@@ -97,3 +97,7 @@ def test_roofline_of_all_and_finest():
     assert r["finest"]["achieved"] == pytest.approx(bpp * 1e9 / (2.0 / 8 * 1e-3) / 1e9, rel=1e-3)
     assert r["finest"]["active_launches_per_step"] == 8
     assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
+    # mean per launch over every launch (the rocprofv3 --stats average)
+    assert r["mean_launch_ms"] == pytest.approx(3.0 / 20, rel=1e-3)
+    assert r["finest"]["mean_launch_ms"] == pytest.approx(2.0 / 10, rel=1e-3)
+    assert r["finest"]["mean_active_launch_ms"] == pytest.approx(2.0 / 8, rel=1e-3)

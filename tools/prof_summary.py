@@ -16,7 +16,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def short(name):
+    """kernel family: template variants of the CG / weighted-median kernels
+    (first launch, odd width; guide channels) are one kernel here"""
     n = name.split("(")[0].replace("void ", "")
+    for fam in ("k_cgp", "k_cgn", "k_cg<", "k_wmf"):
+        if n.startswith(fam):
+            return fam.rstrip("<")
     return n
 
 
@@ -76,21 +81,9 @@ def main():
     out = {}
     H, W = a.H, a.W
 
-    def expected_grid(n):
-        """threads of the finest-level launch (driver.hip grid2 / pair_grid / wmf)"""
-        if n.startswith("k_pcg") or n.startswith("k_sor") or n.startswith("k_norm2"):
-            gx = (W + 127) // 128
-            return gx * 64 * min((H + 3) // 4, max(1, 512 // gx)) * 4
-        if n.startswith("k_wmf"):
-            return ((W + 7) // 8) * 64 * ((H + 7) // 8)
-        gx = (W + 63) // 64
-        return gx * 64 * min((H + 3) // 4, max(1, 2048 // gx)) * 4
-
     for n, lst in names.items():
         tot_ms = sum(sum(v) for _, v in lst) / 1e6
-        eg = expected_grid(n)
-        cand = [gv for gv in lst if gv[0] == eg or gv[0] == eg * 2 or gv[0] == eg * 3]
-        g, v = max(cand, key=lambda gv: len(gv[1])) if cand else max(lst, key=lambda gv: gv[0])
+        g, v = max(lst, key=lambda gv: gv[0])  # finest level: the largest grid
         vs = sorted(v)
         # active (non early-exit) dispatches: the upper half of durations
         act = [x for x in vs if x >= 0.5 * vs[-1]]
@@ -107,8 +100,7 @@ def main():
         hk, mk = Hh.get((n, g), []), M.get((n, g), [])
         if hk and mk and sum(hk) + sum(mk) > 0:
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
-        key = {"k_pcg_iter<true>": "pcg_iter", "k_pcg_iter<false>": "pcg_iter",
-               "k_flow_operator": "flow_operator", "k_wmf<3, 8>": "wmf", "k_rof_iters": "rof_iters",
+        key = {"k_cgp": "pcg_iter", "k_flow_operator": "flow_operator", "k_wmf": "wmf", "k_rof_iters": "rof_iters",
                "k_update_occ": "update_occ", "k_partial_deriv<1>": "partial_deriv_hermite"}.get(n)
         if key in bench.KERNEL_BYTES_PER_PX:
             px = a.H * a.W * (2 if key == "rof_iters" else 1)

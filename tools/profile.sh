@@ -1,18 +1,17 @@
 #!/bin/bash
-# rocprofv3 passes for one bench configuration (run on the GPU box):
-#   1. kernel trace + stats            (durations per dispatch)
-#   2. PMC FETCH_SIZE                  (its own pass: MI355X_MICROARCH.md §rocprofv3)
-#   3. PMC WRITE_SIZE                  (its own pass)
-#   4. PMC TCC_HIT_sum TCC_MISS_sum    (L2 hit rate)
-# usage: tools/profile.sh TAG [bench args...]
+# rocprofv3 passes for the bench (run on the GPU box):
+#   1. kernel trace + stats of the default bench command (durations per dispatch)
+#   2-4. PMC FETCH_SIZE / WRITE_SIZE / TCC hit+miss, each in its own pass
+#        (MI355X_MICROARCH.md rocprofv3 section), on one serial 1080p pair
+# usage: tools/profile.sh TAG
 set -u
 TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-profile $*"
-KRE='cg|wmf|flow_operator|partial_deriv|rof|minmax|update_occ|median|f2_to_planar'
-tools/gpu_step.sh 300 $OUT/trace.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace -- python3 $B || exit $?
-tools/gpu_step.sh 600 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $B || exit $?
-tools/gpu_step.sh 600 $OUT/write.log rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o write -- python3 $B || exit $?
-tools/gpu_step.sh 600 $OUT/l2.log rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT -o l2 -- python3 $B || exit $?
+S="bench.py --steps 1 --warmup 0 --pairs 1 --lanes 1 --no-cpu-baseline --no-profile"
+KRE='k_cgp|k_wmf|k_flow_operator|k_partial_deriv|k_rof_iters|k_update_occ'
+tools/gpu_step.sh 400 $OUT/trace.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace -- python3 bench.py || exit $?
+tools/gpu_step.sh 300 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $S || exit $?
+tools/gpu_step.sh 300 $OUT/write.log rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o write -- python3 $S || exit $?
+tools/gpu_step.sh 300 $OUT/l2.log rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT -o l2 -- python3 $S || exit $?
