@@ -125,6 +125,7 @@ struct of_ctx {
     int slot;
     double px;
     of_stats *st;
+    const char *name;
   };
   std::vector<PendingSolve> pend;
   double *d_partials = nullptr;
@@ -474,6 +475,7 @@ struct SolveResult {
   double rel;
   int slot = -1;  // >= 0: CG solve whose state is still in flight (h_ring[slot])
   double px = 0;
+  const char *name = nullptr;  // fused CG kernel whose active launches profiling counts
 };
 
 // grid for the 2-pixels-per-thread solver kernels, <= PCG_MAX_BLOCKS blocks
@@ -621,6 +623,53 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     // 'backslash' runs the Neumann-preconditioned kernel (k_cgn, 120-column
     // strips), 'pcg' scipy's Jacobi CG (k_cg, 124-column strips)
     const int deg = block ? cg_poly_degree() : 0;
+    // Chebyshev interval of the block-Jacobi-scaled spectrum; OF_CG_CHEB_A
+    // overrides the lower end (A/B measurements)
+    static const double cheb_a = getenv("OF_CG_CHEB_A") ? atof(getenv("OF_CG_CHEB_A")) : 0.04;
+    float poly[4] = {0.f, 0.f, 0.f, 0.f};
+    if (block) {
+      double cb[4];
+      cheb_poly(3, cheb_a, 2.0, cb);
+      for (int i = 0; i < 4; ++i) poly[i] = (float)cb[i];
+    }
+    // ring slot of this solve; a slot is reused only after a synchronisation
+    // has drained its previous solve
+    if ((int)c->pend.size() >= OF_SOLVE_RING - 1) {
+      HIPCHK(hipStreamSynchronize(c->stream));
+      drain_solves(c);
+    }
+    const int slot = c->ring_next;
+    c->ring_next = (slot + 1) % OF_SOLVE_RING;
+    SolveResult res{0, 0, 0.0};
+    res.slot = slot;
+    res.px = (double)H * W;
+    // coarse levels: the whole solve in one workgroup (k_cg_small);
+    // OF_CG_SMALL_PX overrides the size limit (A/B measurements)
+    static const double small_px = getenv("OF_CG_SMALL_PX") ? atof(getenv("OF_CG_SMALL_PX")) : CG_SMALL_PX;
+    if ((double)H * W <= small_px) {
+      CgSmallArgs a;
+      a.coef = coef.p;
+      a.ps = ps;
+      a.b = b.p;
+      a.x = x.p;
+      a.r = new_f2(c, H, W).p;
+      a.p = new_f2(c, H, W).p;
+      a.q = new_f2(c, H, W).p;
+      a.y = new_f2(c, H, W).p;
+      a.t = new_f2(c, H, W).p;
+      a.H = H;
+      a.W = W;
+      a.P = b.P;
+      a.rtol = block ? P->exact_rtol : P->pcg_rtol;
+      a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
+      for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
+      a.st = c->d_state;
+      launch(c, "pcg_small", block ? k_cg_small<3, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY), 0,
+             a);
+      HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+      return res;
+    }
+    res.name = "pcg_iter";
     const int sw = deg == 3 ? PCG_SWP : deg == 1 ? PCG_SWN : PCG_SW;
     const int nstrips = (W + sw - 1) / sw;
     // waves per launch: k_cgp (1 wave per SIMD, LDS ring) fills all 256 CUs
@@ -663,22 +712,8 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       ak.p_new = pb[cur].p;
       return ak;
     };
-    if (deg == 3) {
-      // Chebyshev interval of the block-Jacobi-scaled spectrum; OF_CG_CHEB_A
-      // overrides the lower end (A/B measurements)
-      static const double cheb_a = getenv("OF_CG_CHEB_A") ? atof(getenv("OF_CG_CHEB_A")) : 0.04;
-      double cb[4];
-      cheb_poly(3, cheb_a, 2.0, cb);
-      for (int i = 0; i < 4; ++i) a.poly[i] = (float)cb[i];
-    }
-    // ring slot of this solve; a slot is reused only after a synchronisation
-    // has drained its previous solve
-    if ((int)c->pend.size() >= OF_SOLVE_RING - 1) {
-      HIPCHK(hipStreamSynchronize(c->stream));
-      drain_solves(c);
-    }
-    const int slot = c->ring_next;
-    c->ring_next = (slot + 1) % OF_SOLVE_RING;
+    if (deg == 3)
+      for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
     a.hflag = c->d_flag + slot;
     const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
@@ -692,10 +727,7 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
     HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-    SolveResult r{0, 0, 0.0};
-    r.slot = slot;
-    r.px = (double)H * W;
-    return r;
+    return res;
   }
   // red-black block SOR
   Grid2 g = grid2(H, W, PCG_MAX_BLOCKS);
@@ -747,13 +779,13 @@ void drain_solves(of_ctx *c) {
   for (const auto &p : c->pend) {
     const SolveResult r = resolved(c, p.slot);
     note_solve_now(p.st, r);
-    note_active(c, "pcg_iter", r.iters + 1, p.px);
+    if (p.name) note_active(c, p.name, r.iters + 1, p.px);
   }
   c->pend.clear();
 }
 
 void note_solve(of_ctx *c, of_stats *st, const SolveResult &r) {
-  if (r.slot >= 0) c->pend.push_back({r.slot, r.px, st});
+  if (r.slot >= 0) c->pend.push_back({r.slot, r.px, st, r.name});
   else note_solve_now(st, r);
 }
 
@@ -1628,7 +1660,7 @@ int of_solve(of_ctx *c, const of_params *P, const float *coef, const float *rhs,
   download_f2(c, xx, x);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (r.slot >= 0) {
-    note_active(c, "pcg_iter", resolved(c, r.slot).iters + 1, r.px);
+    if (r.name) note_active(c, r.name, resolved(c, r.slot).iters + 1, r.px);
     r = resolved(c, r.slot);
   }
   if (iters) *iters = r.iters;

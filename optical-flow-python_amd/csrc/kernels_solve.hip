@@ -964,6 +964,202 @@ __global__ __launch_bounds__(256) void k_cgp(PcgArgs g, int k, int R, int nbands
   write_partials<5>(acc, g.part, lds);
 }
 
+// ---------------------------------------------------------------------------
+// k_cg_small: a whole CG solve in ONE workgroup, for levels of at most
+// CG_SMALL_PX pixels.  At the coarse pyramid levels a fused k_cgp launch is
+// latency-bound (~23 us however few rows: its 7-stage row pipeline is walked
+// by one wave per band), and a solve is one launch per iteration; here the
+// whole solve is one launch.  Textbook preconditioned CG with the control
+// flow of scipy.sparse.linalg.cg (base.py:116-136): x0 = 0, stop when
+// ||r|| < rtol ||b|| before an iteration, at most maxiter iterations.
+// Preconditioner as in the fused kernels: DEG 3 = k_cgp's Chebyshev
+// polynomial in the 2x2 block-Jacobi splitting A = D - N (Horner, three
+// neighbour sums), DEG 0 = D^-1 (2x2 blocks if BLOCK, else scipy's scalar
+// Jacobi).  Vectors live in global memory (L2-resident at these sizes);
+// sweeps are separated by workgroup barriers; reductions are fixed-order fp64.
+#define CGS_BX 64
+#define CGS_BY 16
+#define CG_SMALL_PX 4096
+
+struct CgSmallArgs {
+  const float *coef;  // 7 planes, plane stride ps
+  size_t ps;
+  const float2 *b;
+  float2 *x, *r, *p, *q, *y, *t;
+  int H, W, P;
+  double rtol;
+  int maxiter;
+  float poly[4];
+  PcgState *st;
+};
+
+template <bool BLOCK>
+__device__ __forceinline__ void cgs_inv(const float *cf, size_t ps, size_t k, float &ia, float &ic, float &id) {
+  const float a = cf[4 * ps + k], cc = cf[5 * ps + k], d = cf[6 * ps + k];
+  ia = fabsf(a) > 1e-12f ? __builtin_amdgcn_rcpf(a) : 0.f;  // base.py:129-131
+  id = fabsf(d) > 1e-12f ? __builtin_amdgcn_rcpf(d) : 0.f;
+  ic = 0.f;
+  if (BLOCK) {
+    const float det = a * d - cc * cc;
+    const bool ok = det > 1e-30f * fabsf(a * d);
+    const float inv = __builtin_amdgcn_rcpf(det);
+    ia = ok ? d * inv : ia;
+    id = ok ? a * inv : id;
+    ic = ok ? -cc * inv : 0.f;
+  }
+}
+template <bool BLOCK>
+__device__ __forceinline__ float2 cgs_minv(const float *cf, size_t ps, size_t k, float2 f) {
+  float ia, ic, id;
+  cgs_inv<BLOCK>(cf, ps, k, ia, ic, id);
+  return make_float2(ia * f.x + ic * f.y, ic * f.x + id * f.y);
+}
+// (N f)(i, j): edge weight x neighbour value over the 4 neighbours, u and v
+__device__ __forceinline__ float2 cgs_nsum(const float *cf, size_t ps, const float2 *f, int i, int j, int H, int W,
+                                           int P) {
+  const size_t k = (size_t)i * P + j;
+  float su = 0.f, sv = 0.f;
+  if (j > 0) {
+    const float2 n = f[k - 1];
+    su += cf[k - 1] * n.x;
+    sv += cf[2 * ps + k - 1] * n.y;
+  }
+  if (j + 1 < W) {
+    const float2 n = f[k + 1];
+    su += cf[k] * n.x;
+    sv += cf[2 * ps + k] * n.y;
+  }
+  if (i > 0) {
+    const float2 n = f[k - P];
+    su += cf[ps + k - P] * n.x;
+    sv += cf[3 * ps + k - P] * n.y;
+  }
+  if (i + 1 < H) {
+    const float2 n = f[k + P];
+    su += cf[ps + k] * n.x;
+    sv += cf[3 * ps + k] * n.y;
+  }
+  return make_float2(su, sv);
+}
+// fixed-order fp64 sum over the workgroup, returned to every thread
+__device__ __forceinline__ double cgs_sum(double v, double *lds) {
+  const int tid = threadIdx.x + threadIdx.y * CGS_BX;
+  v = wave_sum(v);
+  if ((tid & 63) == 0) lds[tid >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < CGS_BX * CGS_BY / 64; ++w) s += lds[w];
+  __syncthreads();
+  return s;
+}
+
+#define CGS_FOR_PIXELS(H, W)                                  \
+  for (int i = threadIdx.y; i < (H); i += CGS_BY)             \
+    for (int j = threadIdx.x; j < (W); j += CGS_BX)
+
+template <int DEG, bool BLOCK>
+__global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
+  __shared__ double lds[CGS_BX * CGS_BY / 64];
+  const int H = g.H, W = g.W, P = g.P;
+  const size_t ps = g.ps;
+  const float *cf = g.coef;
+  double acc = 0.0;
+  CGS_FOR_PIXELS(H, W) {
+    const size_t k = (size_t)i * P + j;
+    const float2 bb = g.b[k];
+    g.x[k] = make_float2(0.f, 0.f);
+    g.r[k] = bb;
+    g.p[k] = make_float2(0.f, 0.f);
+    acc += (double)(bb.x * bb.x + bb.y * bb.y);
+  }
+  double rr = cgs_sum(acc, lds);
+  const double bnorm = sqrt(rr), atol = g.rtol * bnorm;
+  double rho_prev = 1.0;
+  int it = 0, done = 0;
+  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
+  for (;; ++it) {
+    if (rr == 0.0 && it == 0) { done = 3; break; }
+    if (sqrt(rr) < atol) { done = 1; break; }
+    if (it >= g.maxiter) { done = 2; break; }
+    // z = M^-1 r (into t), rho = r.z
+    acc = 0.0;
+    if (DEG == 0) {
+      CGS_FOR_PIXELS(H, W) {
+        const size_t k = (size_t)i * P + j;
+        const float2 rk = g.r[k], z = cgs_minv<BLOCK>(cf, ps, k, rk);
+        g.t[k] = z;
+        acc += (double)(rk.x * z.x + rk.y * z.y);
+      }
+    } else {
+      CGS_FOR_PIXELS(H, W) {
+        const size_t k = (size_t)i * P + j;
+        g.y[k] = cgs_minv<BLOCK>(cf, ps, k, g.r[k]);
+      }
+      __syncthreads();
+      CGS_FOR_PIXELS(H, W) {  // g2 = c2 y + c3 D^-1 N y
+        const size_t k = (size_t)i * P + j;
+        const float2 ny = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.y, i, j, H, W, P)), yk = g.y[k];
+        g.t[k] = make_float2(c2 * yk.x + c3 * ny.x, c2 * yk.y + c3 * ny.y);
+      }
+      __syncthreads();
+      CGS_FOR_PIXELS(H, W) {  // g1 = c1 y + D^-1 N g2
+        const size_t k = (size_t)i * P + j;
+        const float2 ng = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.t, i, j, H, W, P)), yk = g.y[k];
+        g.q[k] = make_float2(c1 * yk.x + ng.x, c1 * yk.y + ng.y);
+      }
+      __syncthreads();
+      CGS_FOR_PIXELS(H, W) {  // z = c0 y + D^-1 N g1
+        const size_t k = (size_t)i * P + j;
+        const float2 ng = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.q, i, j, H, W, P)), yk = g.y[k];
+        const float2 z = make_float2(c0 * yk.x + ng.x, c0 * yk.y + ng.y), rk = g.r[k];
+        g.t[k] = z;
+        acc += (double)(rk.x * z.x + rk.y * z.y);
+      }
+    }
+    const double rho = cgs_sum(acc, lds);  // (barrier: t complete)
+    const float beta = it == 0 ? 0.f : (float)(rho / rho_prev);
+    CGS_FOR_PIXELS(H, W) {
+      const size_t k = (size_t)i * P + j;
+      const float2 z = g.t[k], pk = g.p[k];
+      g.p[k] = make_float2(z.x + beta * pk.x, z.y + beta * pk.y);
+    }
+    __syncthreads();
+    acc = 0.0;
+    CGS_FOR_PIXELS(H, W) {  // q = A p = D p - N p
+      const size_t k = (size_t)i * P + j;
+      const float2 pk = g.p[k], np = cgs_nsum(cf, ps, g.p, i, j, H, W, P);
+      const float a = cf[4 * ps + k], cc = cf[5 * ps + k], d = cf[6 * ps + k];
+      const float2 qk = make_float2(a * pk.x + cc * pk.y - np.x, cc * pk.x + d * pk.y - np.y);
+      g.q[k] = qk;
+      acc += (double)(pk.x * qk.x + pk.y * qk.y);
+    }
+    const double pq = cgs_sum(acc, lds);
+    const float alpha = (float)(rho / pq);
+    acc = 0.0;
+    CGS_FOR_PIXELS(H, W) {
+      const size_t k = (size_t)i * P + j;
+      const float2 pk = g.p[k], qk = g.q[k], xk = g.x[k], rk = g.r[k];
+      g.x[k] = make_float2(xk.x + alpha * pk.x, xk.y + alpha * pk.y);
+      const float2 rn = make_float2(rk.x - alpha * qk.x, rk.y - alpha * qk.y);
+      g.r[k] = rn;
+      acc += (double)(rn.x * rn.x + rn.y * rn.y);
+    }
+    rr = cgs_sum(acc, lds);
+    rho_prev = rho;
+  }
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    g.st->iter = it;
+    g.st->done = done;
+    g.st->rr = rr;
+    g.st->bnorm = bnorm;
+    g.st->atol = atol;
+  }
+}
+template __global__ void k_cg_small<3, true>(CgSmallArgs);
+template __global__ void k_cg_small<0, true>(CgSmallArgs);
+template __global__ void k_cg_small<0, false>(CgSmallArgs);
+
 // after the last enqueued iteration: apply the convergence test to the last
 // iterate and record the final state (1 block)
 __global__ __launch_bounds__(256) void k_pcg_check(PcgArgs g, int k) {

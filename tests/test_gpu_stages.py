@@ -191,3 +191,50 @@ def test_median_filter(golden):
     np.testing.assert_allclose(median_filter2(d["a"], 5), d["a_med"], atol=1e-6)
     np.testing.assert_allclose(median_filter2(d["t"], 5), d["t_med"], atol=1e-6)
     np.testing.assert_allclose(median_filter2(d["a"], 3), d["a3"], atol=1e-6)
+
+
+def _spd_flow_system(H, W, seed):
+    """A random flow system of the shape flow_operator assembles: positive
+    edge weights spanning 4 decades (robust IRLS weights), PSD 2x2 data blocks,
+    diagonal = data block + sum of incident edge weights."""
+    from optical_flow.methods.base import planes_to_sparse
+    rng = np.random.default_rng(seed)
+    coef = np.zeros((7, H, W))
+    for pl in range(4):
+        coef[pl] = 10.0 ** rng.uniform(-2, 2, (H, W))
+    coef[0][:, -1] = coef[2][:, -1] = 0.0   # no edge right of the last column
+    coef[1][-1, :] = coef[3][-1, :] = 0.0   # nor below the last row
+    ix, iy = rng.normal(0, 3, (H, W)), rng.normal(0, 3, (H, W))
+    psi = 10.0 ** rng.uniform(-1, 1, (H, W))
+    deg = [coef[2 * c].copy() + coef[2 * c + 1] for c in range(2)]
+    for c in range(2):
+        deg[c][:, 1:] += coef[2 * c][:, :-1]
+        deg[c][1:, :] += coef[2 * c + 1][:-1, :]
+    coef[4] = psi * ix * ix + deg[0]
+    coef[5] = psi * ix * iy
+    coef[6] = psi * iy * iy + deg[1]
+    return planes_to_sparse(coef), rng.normal(0, 1, 2 * H * W)
+
+
+@pytest.mark.parametrize("H,W", [(17, 30), (40, 56), (64, 96), (150, 200)])
+def test_solve_synthetic_both_cg_paths(H, W):
+    """'backslash' and 'pcg' on systems below (one-workgroup k_cg_small) and
+    above (fused k_cgp / k_cg launches) the coarse-level size limit
+    (CG_SMALL_PX = 4096 px): 'backslash' to <= 1e-4 relative error of the
+    direct solve, 'pcg' within 2e-2 of scipy cg (Jacobi, rtol 1e-3)."""
+    from optical_flow.methods.config import load_of_method
+    from scipy.sparse.linalg import spsolve, cg, LinearOperator
+    A, b = _spd_flow_system(H, W, seed=H * W)
+    o = load_of_method("classic+nl-fast")
+
+    def flat(x):
+        return np.concatenate([x[..., 0].ravel(order="F"), x[..., 1].ravel(order="F")])
+
+    xr = spsolve(A.tocsc(), b)
+    x = flat(o._solve_linear_system(A, b, (H, W, 2)))
+    assert np.linalg.norm(x - xr) <= 1e-4 * np.linalg.norm(xr), np.linalg.norm(x - xr) / np.linalg.norm(xr)
+    dg = A.diagonal()
+    xs, _ = cg(A, b, M=LinearOperator(A.shape, matvec=lambda v: v / dg), maxiter=200, rtol=1e-3)
+    o.solver = "pcg"
+    x = flat(o._solve_linear_system(A, b, (H, W, 2)))
+    assert np.linalg.norm(x - xs) <= 2e-2 * np.linalg.norm(xs), np.linalg.norm(x - xs) / np.linalg.norm(xs)
