@@ -85,14 +85,18 @@ def main():
         tot_ms = sum(sum(v) for _, v in lst) / 1e6
         g, v = max(lst, key=lambda gv: gv[0])  # finest level: the largest grid
         vs = sorted(v)
-        # active (non early-exit) dispatches: the upper half of durations
-        act = [x for x in vs if x >= 0.5 * vs[-1]]
-        mean_us = sum(act) / len(act) / 1e3
-        rec = {"total_ms": round(tot_ms, 3), "finest_grid": g, "finest_calls": len(v), "finest_mean_us": round(mean_us, 2)}
+        # active (non early-exit) dispatches: at least half the median
+        # duration; the median is robust to dispatches slowed by a concurrent
+        # lane's kernels
+        med = vs[len(vs) // 2]
+        act = [x for x in vs if x >= 0.5 * med]
+        mean_us = act[len(act) // 2] / 1e3
+        rec = {"total_ms": round(tot_ms, 3), "finest_grid": g, "finest_calls": len(v), "finest_active_calls": len(act),
+               "finest_median_us": round(mean_us, 2), "all_mean_us": round(tot_ms * 1e3 / sum(len(x) for _, x in lst), 2)}
         fk = [x for x in F.get((n, g), []) if x > 0]
         wk = [x for x in Wr.get((n, g), []) if x > 0]
         if fk:
-            fk = sorted(fk)[len(fk) // 2:]  # active dispatches
+            fk = sorted(fk)[len(fk) // 2:]  # active dispatches (no-op CG launches fetch ~nothing)
             rec["fetch_MB"] = round(sum(fk) / len(fk) * 1024 / 1e6, 3)
         if wk:
             wk = sorted(wk)[len(wk) // 2:]
