@@ -687,6 +687,20 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       gyb = (nbands + 3) / 4;
     }
     dim3 grid(nstrips, gyb), blk(OF_BX, OF_BY);
+    // 'backslash' default: k_cgs (the degree-3 iteration with its stages split
+    // over a block's 4 waves, one band per block, 2 blocks per CU);
+    // OF_CG_KERNEL=cgp selects k_cgp (A/B measurements)
+    static const bool use_cgp = getenv("OF_CG_KERNEL") && !strcmp(getenv("OF_CG_KERNEL"), "cgp");
+    const bool split = deg == 3 && !use_cgp;
+    if (split) {
+      static const int blocks_env = getenv("OF_CGS_BLOCKS") ? atoi(getenv("OF_CGS_BLOCKS")) : 0;
+      const int target = blocks_env > 0 ? std::min(blocks_env, PCG_MAX_BLOCKS) : 512;
+      nbands = std::max(1, std::min((H + 7) / 8, target / nstrips));
+      R = (H + nbands - 1) / nbands;
+      nbands = (H + R - 1) / R;
+      grid = dim3(nstrips, nbands);
+      gyb = nbands;
+    }
     PcgArgs a;
     memset(&a, 0, sizeof(a));
     a.coef = coef.p;
@@ -717,7 +731,9 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     a.hflag = c->d_flag + slot;
     const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
-      auto kern = deg == 3 ? (k == 0 ? (odd ? k_cgp<true, true> : k_cgp<true, false>)
+      auto kern = split ? (k == 0 ? (odd ? k_cgs<true, true> : k_cgs<true, false>)
+                                  : (odd ? k_cgs<false, true> : k_cgs<false, false>))
+                  : deg == 3 ? (k == 0 ? (odd ? k_cgp<true, true> : k_cgp<true, false>)
                                      : (odd ? k_cgp<false, true> : k_cgp<false, false>))
                   : deg == 1 ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
                                        : (odd ? k_cgn<false, true> : k_cgn<false, false>))

@@ -1160,6 +1160,289 @@ template __global__ void k_cg_small<3, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, false>(CgSmallArgs);
 
+// ---------------------------------------------------------------------------
+// k_cgs: k_cgp's iteration (same preconditioner, same rho recurrence, same
+// per-element arithmetic) with its pipeline stages split over the 4 waves of
+// a block, which all work on ONE band:
+//   wave 0: loads, coefficient records -> LDS ring, A) r, y of row n-1
+//   wave 1: B) g2 of row n-3, C) g1 of row n-4
+//   wave 2: D) z, p, x of row n-6, E) q, y_q of row n-7
+//   wave 3: F) v1 and the T terms of row n-9
+// with one block barrier per row step; rows cross waves through small LDS
+// rings (y, g1, y_q; records in a 12-row ring), a wave's own rows stay in
+// registers.  k_cgp gives each wave its own band and the whole pipeline, so
+// a band of R rows costs R + 12 steps of all 6 stages per wave and its
+// 32-KB record ring allows one wave per SIMD (R = 20 at 1080p: 1.6x the rows
+// read); here 64 KB of LDS per block allow 2 blocks per CU (R = 39 at
+// 1080p, 1.36x) and a step costs only the heaviest wave's share.
+// Stage lags follow from one barrier per step: a stage reads rows of another
+// wave produced at earlier steps; the band is walked for n in
+// [r0 - 5, r1 + 8] so that every row a required stage reads was produced.
+#define CGS_NREC 12
+
+template <bool FIRST, bool ODD>
+__global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands) {
+  __shared__ double lds[64];
+  __shared__ float4 ring[CGS_NREC][4][64];  // [row slot][record quarter][lane]
+  __shared__ float4 s_y[8][64], s_g1[4][64], s_yq[4][64];
+  const int H = g.H, W = g.W;
+  const unsigned rowb4 = (unsigned)g.P * 4u, rowb8 = (unsigned)g.P * 8u;
+  const size_t vbytes = (size_t)H * g.P * 8;
+  const __amdgpu_buffer_rsrc_t rc = cg_rsrc(g.coef, g.ps * 7 * 4);
+  const __amdgpu_buffer_rsrc_t rin = cg_rsrc(FIRST ? g.b : g.r_in, vbytes);
+  const __amdgpu_buffer_rsrc_t rpo = cg_rsrc(g.p_old, vbytes);
+  const __amdgpu_buffer_rsrc_t rx = cg_rsrc(g.x, vbytes);
+  const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
+  const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
+  const unsigned ps4 = (unsigned)(g.ps * 4);
+  const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = blockIdx.y;
+  const int tid = lane + wid * 64;
+  const int jc = blockIdx.x * PCG_SWP - 8 + 2 * lane;
+  const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
+  const bool out_lane = lane >= 4 && lane <= 59;
+  const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
+  const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
+  const bool live = band < nbands;
+  const int r0 = band * R, r1 = min(r0 + R, H);
+  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
+  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb4 : CG_ROW_OOB); };
+  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb8 : CG_ROW_OOB); };
+  auto load_raw = [&](int t, CgRaw &c) {
+    const unsigned v = o4(t);
+    c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
+    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
+    c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
+    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
+    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
+    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
+    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
+  };
+  // records are keyed by absolute row (rows >= r0 - 7 >= -7)
+  auto rslot = [](int t) { return (t + 2 * CGS_NREC) % CGS_NREC; };
+  auto put_rec = [&](int t, const CgRaw &c) {
+    CgCoef cc;
+    cc.a = c.a;
+    cc.c = c.c;
+    cc.d = c.d;
+    const CgInv mi = cg_inv<true>(cc);
+    float4 *q = &ring[rslot(t)][0][lane];
+    q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
+    q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
+    q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
+    q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
+  };
+  auto get_rec = [&](int t) {
+    const float4 *q = &ring[rslot(t)][0][lane];
+    const float4 a = q[0], b = q[64], c = q[128], d = q[192];
+    CgRec r;
+    r.wx[0] = cg_f2{a.x, a.y};
+    r.wy[0] = cg_f2{a.z, a.w};
+    r.wx[1] = cg_f2{b.x, b.y};
+    r.wy[1] = cg_f2{b.z, b.w};
+    r.ma[0] = cg_f2{c.x, c.y};
+    r.mb[0] = cg_f2{c.z, c.w};
+    r.ma[1] = cg_f2{d.x, d.y};
+    r.mb[1] = cg_f2{d.z, d.w};
+    return r;
+  };
+  auto get_wy = [&](int t, cg_f2 (&wu)[2]) {  // vertical weight pairs only
+    const float2 *q = reinterpret_cast<const float2 *>(&ring[rslot(t)][0][lane]);
+    const float2 a = q[1], b = q[129];
+    wu[0] = cg_f2{a.x, a.y};
+    wu[1] = cg_f2{b.x, b.y};
+  };
+  auto ld4 = [&](float4 (&rg)[4][64], int t) {
+    const float4 v = rg[t & 3][lane];
+    return cg_f4{v.x, v.y, v.z, v.w};
+  };
+  auto st4 = [&](float4 (&rg)[4][64], int t, cg_f4 v) { rg[t & 3][lane] = make_float4(v.x, v.y, v.z, v.w); };
+  auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
+  auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
+  auto load_x = [&](int t) {
+    return (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
+  };
+  const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;
+  auto mdot = [&](cg_f4 a, cg_f4 b) {
+    const cg_f2 p = cg_lo(a) * cg_lo(b), q = cg_hi(a) * cg_hi(b);
+    return (dm0 ? p.x + p.y : 0.f) + (dm1 ? q.x + q.y : 0.f);
+  };
+  const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const int ns = r0 - 5, ne = r1 + 8;
+
+  // zeroed rings: rows above the band that no required stage reads
+  {
+    float4 *z = &ring[0][0][0];
+    for (int e = tid; e < CGS_NREC * 4 * 64; e += 256) z[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = tid; e < 8 * 64; e += 256) (&s_y[0][0])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = tid; e < 4 * 64; e += 256) {
+      (&s_g1[0][0])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      (&s_yq[0][0])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // wave 0: raw rows ns-2 .. ns+1, p_old rows ns-2 .. ns+1, r_in row ns-1
+  // wave 2: p_old, x of row ns-6 (register rings indexed by (row - ns))
+  CgRaw SG[4], SGp[2];
+  cg_f4 PO[8], RI[2], PO2[2], XI[2];
+  if (live && wid == 0) {
+    load_raw(ns - 2, SGp[0]);
+    load_raw(ns - 1, SGp[1]);
+    load_raw(ns, SG[0]);
+    load_raw(ns + 1, SG[1]);
+#pragma unroll
+    for (int m = -2; m <= 1; ++m) PO[m & 7] = load_po(ns + m);
+    RI[1] = load_rin(ns - 1);
+  }
+  if (live && wid == 2) {
+    PO2[0] = load_po(ns - 6);
+    XI[0] = load_x(ns - 6);
+  }
+  float alpha = 0.f, beta = 0.f;
+  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
+
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    if (wid == 0) {
+      put_rec(ns - 2, SGp[0]);
+      put_rec(ns - 1, SGp[1]);
+    }
+    __syncthreads();
+    // each wave runs its own role's loop (registers of one role only), one
+    // block barrier per row step in every role (same step count)
+#define CGS_STEPS(...)                                                    \
+  for (int n0 = ns; n0 <= ne; n0 += 8) {                                  \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                       \
+      const int n = n0 + u;                                               \
+      if (n > ne) break;                                                  \
+      __VA_ARGS__                                                         \
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");              \
+      __builtin_amdgcn_s_barrier();                                       \
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");              \
+    }                                                                     \
+  }
+// register-ring index of row n + d: (u + d) mod ring size
+#define R8(d) ((u + (d) + 16) & 7)
+#define R4(d) ((u + (d) + 16) & 3)
+#define R2(d) ((u + (d) + 16) & 1)
+    if (wid == 0) {
+      CGS_STEPS({
+        load_raw(n + 2, SG[R4(2)]);
+        PO[R8(2)] = load_po(n + 2);
+        RI[R2(0)] = load_rin(n);
+        put_rec(n, SG[R4(0)]);
+        // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
+        const CgRec q1 = get_rec(n - 1);
+        cg_f2 wu[2];
+        get_wy(n - 2, wu);
+        cg_f4 r = RI[R2(-1)];
+        if (!FIRST) r -= alpha * (cgr_diag(q1, PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
+        const cg_f4 y = cgr_minv(q1, r);
+        s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
+        const int o = n - 1;
+        if (o >= r0 && o < r1) {
+          cg_st4(rro, soff8 + (unsigned)o * rowb8, r);
+          acc[4] += (double)mdot(r, r);
+          acc[3] += (double)(c0 * mdot(r, y));
+        }
+      })
+    } else if (wid == 1) {
+      cg_f4 G2[4] = {zero4, zero4, zero4, zero4};
+      CGS_STEPS({
+        // B) row n-3: g2 = c2 y + c3 D^-1 N y
+        {
+          const CgRec q2 = get_rec(n - 3);
+          cg_f2 wu[2];
+          get_wy(n - 4, wu);
+          const float4 a = s_y[(n - 4) & 7][lane], b = s_y[(n - 3) & 7][lane], c = s_y[(n - 2) & 7][lane];
+          const cg_f4 ym = {a.x, a.y, a.z, a.w}, y0 = {b.x, b.y, b.z, b.w}, yp = {c.x, c.y, c.z, c.w};
+          const cg_f4 ny = cgr_nsum(ym, y0, yp, q2, wu);
+          G2[R4(-3)] = c2 * y0 + c3 * cgr_minv(q2, ny);
+        }
+        // C) row n-4: g1 = c1 y + D^-1 N g2
+        {
+          const CgRec q3 = get_rec(n - 4);
+          cg_f2 wu[2];
+          get_wy(n - 5, wu);
+          const float4 b = s_y[(n - 4) & 7][lane];
+          const cg_f4 y0 = {b.x, b.y, b.z, b.w};
+          const cg_f4 ng = cgr_nsum(G2[R4(-5)], G2[R4(-4)], G2[R4(-3)], q3, wu);
+          st4(s_g1, n - 4, c1 * y0 + cgr_minv(q3, ng));
+        }
+      })
+    } else if (wid == 2) {
+      cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
+      CGS_STEPS({
+        PO2[R2(-5)] = load_po(n - 5);
+        XI[R2(-5)] = load_x(n - 5);
+        // D) row n-6: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
+        {
+          const CgRec q4 = get_rec(n - 6);
+          cg_f2 wu[2];
+          get_wy(n - 7, wu);
+          const cg_f4 ng = cgr_nsum(ld4(s_g1, n - 7), ld4(s_g1, n - 6), ld4(s_g1, n - 5), q4, wu);
+          const float4 b = s_y[(n - 6) & 7][lane];
+          const cg_f4 yr = {b.x, b.y, b.z, b.w};
+          const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
+          cg_f4 p = FIRST ? z : z + beta * PO2[R2(-6)];
+          const int o = n - 6;
+          const bool rv = (unsigned)o < (unsigned)H;
+          if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
+          if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
+          PP[R4(-6)] = p;
+          ZZ[R2(-6)] = z;
+          if (o >= r0 && o < r1) {
+            const unsigned so = soff8 + (unsigned)o * rowb8;
+            cg_st4(rpn, so, p);
+            cg_st4(rx, so, FIRST ? zero4 : XI[R2(-6)] + alpha * PO2[R2(-6)]);
+            acc[3] += (double)mdot(yr, ng);
+          }
+        }
+        // E) row n-7: q = A p, y_q = D^-1 q
+        {
+          const CgRec q5 = get_rec(n - 7);
+          cg_f2 wu[2];
+          get_wy(n - 8, wu);
+          const cg_f4 pm = PP[R4(-7)];
+          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[R4(-8)], pm, PP[R4(-6)], q5, wu);
+          const cg_f4 yq = cgr_minv(q5, q);
+          st4(s_yq, n - 7, yq);
+          const int o = n - 7;
+          if (o >= r0 && o < r1) {
+            acc[0] += (double)mdot(pm, q);
+            acc[1] += (double)mdot(q, ZZ[R2(-7)]);
+            acc[2] += (double)(c0 * mdot(q, yq));
+          }
+        }
+      })
+    } else {
+      cg_f4 V1[2] = {zero4, zero4};
+      CGS_STEPS({
+        // F) row n-9: N y_q, v1 = D^-1 N y_q, T1..T3
+        const CgRec q6 = get_rec(n - 9);
+        cg_f2 wy7[2];
+        get_wy(n - 10, wy7);
+        const cg_f4 yq = ld4(s_yq, n - 9);
+        const cg_f4 ny = cgr_nsum(ld4(s_yq, n - 10), yq, ld4(s_yq, n - 8), q6, wy7);
+        const cg_f4 v1 = cgr_minv(q6, ny);
+        const cg_f4 vu = V1[R2(-10)];
+        V1[R2(-9)] = v1;
+        const int o = n - 9;
+        if (o >= r0 && o < r1) {
+          const cg_f2 v0 = cg_lo(v1), vv1 = cg_hi(v1);
+          const cg_f2 h0 = cg_left2(q6.wx[1]) * cg_left2(vv1) + wy7[0] * cg_lo(vu);
+          const cg_f2 h1 = q6.wx[0] * v0 + wy7[1] * cg_hi(vu);
+          const cg_f4 t = (c1 * yq + c2 * v1) * ny + (2.0f * c3) * v1 * cg_cat(h0, h1);
+          acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
+        }
+      })
+    }
+#undef R8
+#undef R4
+#undef R2
+#undef CGS_STEPS
+  }
+  write_partials<5>(acc, g.part, lds);
+}
+
 // after the last enqueued iteration: apply the convergence test to the last
 // iterate and record the final state (1 block)
 __global__ __launch_bounds__(256) void k_pcg_check(PcgArgs g, int k) {
