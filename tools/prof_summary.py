@@ -19,7 +19,7 @@ def short(name):
     """kernel family: template variants of the CG / weighted-median kernels
     (first launch, odd width; guide channels) are one kernel here"""
     n = name.split("(")[0].replace("void ", "")
-    for fam in ("k_cgp", "k_cgn", "k_cg<", "k_wmf"):
+    for fam in ("k_cgs", "k_cgp", "k_cgn", "k_cg_small", "k_cg<", "k_wmf"):
         if n.startswith(fam):
             return fam.rstrip("<")
     return n
@@ -104,7 +104,7 @@ def main():
         hk, mk = Hh.get((n, g), []), M.get((n, g), [])
         if hk and mk and sum(hk) + sum(mk) > 0:
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
-        key = {"k_cgp": "pcg_iter", "k_flow_operator": "flow_operator", "k_wmf": "wmf", "k_rof_iters": "rof_iters",
+        key = {"k_cgs": "pcg_iter", "k_cgp": "pcg_iter", "k_flow_operator": "flow_operator", "k_wmf": "wmf", "k_rof_iters": "rof_iters",
                "k_update_occ": "update_occ", "k_partial_deriv<1>": "partial_deriv_hermite"}.get(n)
         if key in bench.KERNEL_BYTES_PER_PX:
             px = a.H * a.W * (2 if key == "rof_iters" else 1)

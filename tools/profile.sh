@@ -10,7 +10,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 S="bench.py --steps 1 --warmup 0 --pairs 1 --lanes 1 --no-cpu-baseline --no-profile"
-KRE='k_cgp|k_wmf|k_flow_operator|k_partial_deriv|k_rof_iters|k_update_occ'
+KRE='k_cgs|k_cgp|k_wmf|k_flow_operator|k_partial_deriv|k_rof_iters|k_update_occ'
 tools/gpu_step.sh 400 $OUT/trace.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace -- python3 bench.py || exit $?
 tools/gpu_step.sh 300 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $S || exit $?
 tools/gpu_step.sh 300 $OUT/write.log rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o write -- python3 $S || exit $?
