@@ -219,7 +219,7 @@ def _spd_flow_system(H, W, seed):
 @pytest.mark.parametrize("H,W", [(17, 30), (40, 56), (64, 96), (150, 200)])
 def test_solve_synthetic_both_cg_paths(H, W):
     """'backslash' and 'pcg' on systems below (one-workgroup k_cg_small) and
-    above (fused k_cgp / k_cg launches) the coarse-level size limit
+    above (fused k_cgs / k_cg launches) the coarse-level size limit
     (CG_SMALL_PX = 4096 px): 'backslash' to <= 1e-4 relative error of the
     direct solve, 'pcg' within 2e-2 of scipy cg (Jacobi, rtol 1e-3)."""
     from optical_flow.methods.config import load_of_method
