@@ -200,6 +200,39 @@ int of_rccl_init(of_ctx *ctx, const char *id128, int nranks, int rank);
 int of_rccl_gather_flows(of_ctx *ctx, int nslots, float *out_uv_rank0);
 int of_rccl_finalize(of_ctx *ctx);
 
+/* ---- solver diagnostics ---- */
+/* Launch geometry of the iterative solver kernels for an H x W level (no
+ * device needed): CG ('backslash' k_cgs, 'pcg' k_cg) strips x bands, or the
+ * SOR kernel's 64-row strips (grid_x = 2 * strips).  OF_ENOTSUP when the
+ * level is too large for the kernel (too wide for the partial-sum slots /
+ * too tall for the SOR hand-off words). */
+typedef struct of_cg_geometry {
+  int32_t grid_x, grid_y;  /* launch grid (blocks) */
+  int32_t rows;            /* rows per band */
+  int32_t bands;
+  int32_t blocks;          /* grid_x * grid_y */
+  int32_t strip_cols;      /* output columns per strip */
+} of_cg_geometry;
+int of_solver_geometry(int H, int W, int solver, of_cg_geometry *out);
+
+/* Solve log: with it on, every linear solve (_solve_linear_system,
+ * base.py:87-172) is followed by an fp64 evaluation of its TRUE relative
+ * residual ||b - A x|| / ||b|| from the fp32 operator; records keep the
+ * solver's own estimate beside it (CG: the recurrence residual; SOR: the
+ * last sweep's ||dx|| / ||x||).  Enabling clears the log; at most 4096
+ * records per context.  Diagnostic only: adds two small launches per solve. */
+typedef struct of_solve_record {
+  int32_t h, w;
+  int32_t solver;   /* enum of_solver */
+  int32_t iters;    /* CG iterations / SOR sweeps */
+  int32_t done;     /* 1 converged, 2 iteration limit, 3 zero rhs */
+  int32_t pad_;
+  double true_rel;  /* ||b - A x|| / ||b||, fp64 */
+  double est_rel;
+} of_solve_record;
+int of_set_solve_log(of_ctx *ctx, int enable);
+int of_solve_log(of_ctx *ctx, int max, of_solve_record *out, int *n);
+
 /* ---- stage entries (one per hot-path row of SURVEY.md §8a; parity tests) ---- */
 /* _rgb2gray + _rgb2lab + per-channel scale_image (interface.py:49-64,74-141) */
 int of_preprocess(of_ctx *ctx, const float *rgb1, const float *rgb2, int H, int W,

@@ -106,6 +106,14 @@ struct Slot {
 }  // namespace
 
 #define OF_SOLVE_RING 256
+#define OF_SLOG_MAX 4096  // solve-log entries kept per context
+// lanes mode: phases on levels of at least this many pixels hold the token
+#define OF_BIG_PX (double)(1 << 20)
+// SOR hand-off words: a ticket counter, then [2][SOR_MAXS] progress stamps
+#define OF_SOR_SYNC_BYTES (256 + 2 * SOR_MAXS * sizeof(int))
+// dynamic LDS of a k_sor_lex block: unused, it keeps one block per CU (the
+// measured configuration of the sc1 hand-off, MI355X_MICROARCH.md)
+#define OF_SOR_SHM (96 * 1024)
 
 struct of_ctx {
   int device = 0;
@@ -129,6 +137,15 @@ struct of_ctx {
   };
   std::vector<PendingSolve> pend;
   double *d_partials = nullptr;
+  unsigned *d_sor_sync = nullptr;
+  // solve log (of_set_solve_log): fp64 true residual of every solve
+  int slog = 0;
+  struct SolveLog {
+    int h, w, solver, slot, iters, done;
+    double est;
+  };
+  std::vector<SolveLog> slog_rec;
+  double *d_rpart = nullptr, *d_rlog = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
   int prof = 0;  // 0 off, 1 per kernel, 2 per kernel and level ("name@pixels")
@@ -597,39 +614,62 @@ void cheb_poly(int m, double a, double b, double *cB) {
   }
 }
 
-// 'backslash' CG kernel: 3 = Chebyshev degree-3 polynomial (k_cgp, default),
-// 1 = first-order Neumann (k_cgn); OF_CG_POLY overrides (A/B measurements)
-int cg_poly_degree() {
-  static int d = [] {
-    const char *e = getenv("OF_CG_POLY");
-    return e && atoi(e) == 1 ? 1 : 3;
-  }();
-  return d;
+// Chebyshev interval [CG_CHEB_A, 2] of the block-Jacobi-scaled spectrum
+// D^-1 A of the 'backslash' preconditioner (kernels_solve.hip, k_cgs).  The
+// lower end trades iterations for parity: 0.06 saves 4 % of the iterations
+// but moves the 48x64 smoke pair's mean |uv - oracle| from 6.7e-4 to 6.1e-3
+// (knob sweep).
+#define CG_CHEB_A 0.04
+
+// Launch geometry of the fused CG iteration kernels for an H x W level.
+// k_cg ('pcg'): strips of PCG_SW columns x bands of R rows, 4 bands (waves)
+// per 256-thread block, ~768 waves per launch.  k_cgs ('backslash'): strips
+// of PCG_SWP columns x bands of R rows, one band per block, ~512 blocks (2
+// per CU).  Every block writes one slot of the partials buffer, so the grid
+// may not exceed PCG_MAX_BLOCKS blocks: levels wider than PCG_MAX_BLOCKS
+// strips are refused (OF_ENOTSUP), never silently mis-sized.
+int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
+  if (H < 1 || W < 1) return OF_EINVAL;
+  const int sw = split ? PCG_SWP : PCG_SW;
+  const int nstrips = (W + sw - 1) / sw;
+  if (nstrips > PCG_MAX_BLOCKS) return OF_ENOTSUP;
+  int nbands, R, gy;
+  if (split) {
+    nbands = std::max(1, std::min((H + 7) / 8, PCG_MAX_BLOCKS / nstrips));
+    R = (H + nbands - 1) / nbands;
+    nbands = (H + R - 1) / R;
+    gy = nbands;
+  } else {
+    nbands = std::max(1, std::min((H + 3) / 4, 768 / nstrips));
+    R = (H + nbands - 1) / nbands;
+    nbands = (H + R - 1) / R;
+    gy = (nbands + 3) / 4;
+    while (nstrips * gy > PCG_MAX_BLOCKS) {  // ends: gy = 1 once R >= H / 4
+      ++R;
+      nbands = (H + R - 1) / R;
+      gy = (nbands + 3) / 4;
+    }
+  }
+  g->grid_x = nstrips;
+  g->grid_y = gy;
+  g->rows = R;
+  g->bands = nbands;
+  g->blocks = nstrips * gy;
+  g->strip_cols = sw;
+  return g->blocks <= PCG_MAX_BLOCKS ? OF_OK : OF_ENOTSUP;
 }
 
-SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
   const int H = b.H, W = b.W;
   c->cur_px = (double)H * W;
   const size_t ps = coef.ps();
   const int solver = P->solver;
   if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
     const bool block = solver == OF_SOLVER_BACKSLASH;
-    // fused-iteration geometry: 128-column strips x bands of R rows, 4 bands
-    // per block, <= PCG_MAX_BLOCKS blocks, ~2048 waves when the level allows
-    // fused-iteration geometry: PCG_SW-column strips x bands of R rows, 4
-    // bands per block, <= PCG_MAX_BLOCKS blocks, ~768 waves when the level
-    // allows (measured optimum at 1080p: fewer waves = less halo recompute,
-    // more = more latency hiding)
-    // 'backslash' runs the Neumann-preconditioned kernel (k_cgn, 120-column
-    // strips), 'pcg' scipy's Jacobi CG (k_cg, 124-column strips)
-    const int deg = block ? cg_poly_degree() : 0;
-    // Chebyshev interval of the block-Jacobi-scaled spectrum; OF_CG_CHEB_A
-    // overrides the lower end (A/B measurements)
-    static const double cheb_a = getenv("OF_CG_CHEB_A") ? atof(getenv("OF_CG_CHEB_A")) : 0.04;
     float poly[4] = {0.f, 0.f, 0.f, 0.f};
     if (block) {
       double cb[4];
-      cheb_poly(3, cheb_a, 2.0, cb);
+      cheb_poly(3, CG_CHEB_A, 2.0, cb);
       for (int i = 0; i < 4; ++i) poly[i] = (float)cb[i];
     }
     // ring slot of this solve; a slot is reused only after a synchronisation
@@ -643,10 +683,8 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     SolveResult res{0, 0, 0.0};
     res.slot = slot;
     res.px = (double)H * W;
-    // coarse levels: the whole solve in one workgroup (k_cg_small);
-    // OF_CG_SMALL_PX overrides the size limit (A/B measurements)
-    static const double small_px = getenv("OF_CG_SMALL_PX") ? atof(getenv("OF_CG_SMALL_PX")) : CG_SMALL_PX;
-    if ((double)H * W <= small_px) {
+    // coarse levels: the whole solve in one workgroup (k_cg_small)
+    if ((double)H * W <= CG_SMALL_PX) {
       CgSmallArgs a;
       a.coef = coef.p;
       a.ps = ps;
@@ -670,37 +708,15 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       return res;
     }
     res.name = "pcg_iter";
-    const int sw = deg == 3 ? PCG_SWP : deg == 1 ? PCG_SWN : PCG_SW;
-    const int nstrips = (W + sw - 1) / sw;
-    // waves per launch: k_cgp (1 wave per SIMD, LDS ring) fills all 256 CUs
-    static const int waves_env = getenv("OF_CG_WAVES") ? atoi(getenv("OF_CG_WAVES")) : 0;
-    const int waves = waves_env > 0 ? waves_env : (deg == 3 ? 1024 : 768);
-    REQUIRE(deg != 3 || coef.ps() * 7 * 4 < 0x40000000ull, OF_ENOTSUP, "level too large for the CG kernel");
-    int nbands = std::max(1, std::min((H + 3) / 4, waves / nstrips));
-    int R = (H + nbands - 1) / nbands;
-    nbands = (H + R - 1) / R;
-    int gyb = (nbands + 3) / 4;
-    const int max_blocks = deg == 3 ? 256 : PCG_MAX_BLOCKS;  // k_cgp: one 128-KB-LDS block per CU
-    while (nstrips * gyb > max_blocks) {
-      ++R;
-      nbands = (H + R - 1) / R;
-      gyb = (nbands + 3) / 4;
-    }
-    dim3 grid(nstrips, gyb), blk(OF_BX, OF_BY);
-    // 'backslash' default: k_cgs (the degree-3 iteration with its stages split
-    // over a block's 4 waves, one band per block, 2 blocks per CU);
-    // OF_CG_KERNEL=cgp selects k_cgp (A/B measurements)
-    static const bool use_cgp = getenv("OF_CG_KERNEL") && !strcmp(getenv("OF_CG_KERNEL"), "cgp");
-    const bool split = deg == 3 && !use_cgp;
-    if (split) {
-      static const int blocks_env = getenv("OF_CGS_BLOCKS") ? atoi(getenv("OF_CGS_BLOCKS")) : 0;
-      const int target = blocks_env > 0 ? std::min(blocks_env, PCG_MAX_BLOCKS) : 512;
-      nbands = std::max(1, std::min((H + 7) / 8, target / nstrips));
-      R = (H + nbands - 1) / nbands;
-      nbands = (H + R - 1) / R;
-      grid = dim3(nstrips, nbands);
-      gyb = nbands;
-    }
+    // 'backslash': k_cgs (the degree-3 iteration with its stages split over a
+    // block's 4 waves); 'pcg': scipy's Jacobi CG in k_cg
+    const bool split = block;
+    of_cg_geometry geo;
+    const int gst = cg_geometry(H, W, split, &geo);
+    REQUIRE(gst == OF_OK, gst, "level too wide for the fused CG kernels");
+    REQUIRE(coef.ps() * 7 * 4 < 0x40000000ull, OF_ENOTSUP, "level too large for the CG kernels");
+    const dim3 grid(geo.grid_x, geo.grid_y), blk(OF_BX, OF_BY);
+    const int R = geo.rows, nbands = geo.bands;
     PcgArgs a;
     memset(&a, 0, sizeof(a));
     a.coef = coef.p;
@@ -711,8 +727,7 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
     a.W = W;
     a.P = b.P;
     a.ps = ps;
-    a.nb = nstrips * gyb;
-    a.part = c->d_partials;
+    a.nb = geo.blocks;
     a.st = c->d_state;
     a.rtol = block ? P->exact_rtol : P->pcg_rtol;
     a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
@@ -724,30 +739,32 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
       ak.p_old = pb[prev].p;
       ak.r_out = rb[cur].p;
       ak.p_new = pb[cur].p;
+      ak.part_rd = c->d_partials + (size_t)prev * 5 * PCG_MAX_BLOCKS;
+      ak.part_wr = c->d_partials + (size_t)cur * 5 * PCG_MAX_BLOCKS;
       return ak;
     };
-    if (deg == 3)
-      for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
+    for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
     a.hflag = c->d_flag + slot;
     const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
       auto kern = split ? (k == 0 ? (odd ? k_cgs<true, true> : k_cgs<true, false>)
                                   : (odd ? k_cgs<false, true> : k_cgs<false, false>))
-                  : deg == 3 ? (k == 0 ? (odd ? k_cgp<true, true> : k_cgp<true, false>)
-                                     : (odd ? k_cgp<false, true> : k_cgp<false, false>))
-                  : deg == 1 ? (k == 0 ? (odd ? k_cgn<true, true> : k_cgn<true, false>)
-                                       : (odd ? k_cgn<false, true> : k_cgn<false, false>))
-                             : (k == 0 ? (odd ? k_cg<true, false, true> : k_cg<true, false, false>)
-                                       : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
+                        : (k == 0 ? (odd ? k_cg<true, false, true> : k_cg<true, false, false>)
+                                  : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
     HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     return res;
   }
-  // red-black block SOR
-  Grid2 g = grid2(H, W, PCG_MAX_BLOCKS);
+  // lexicographic SOR (base.py:138-172): one launch per sweep, 64-row strips
+  // of the u half then of the v half (kernels_solve.hip, k_sor_lex)
+  REQUIRE(solver == OF_SOLVER_SOR, OF_EINVAL, "Unknown solver");
+  const int nstrips = (H + 63) / 64;
+  REQUIRE(nstrips <= SOR_MAXS, OF_ENOTSUP, "level too tall for the SOR kernel");
+  REQUIRE(((double)P->sor_max_iters + 2.0) * (W + 64.0) < 2.0e9, OF_ENOTSUP, "sor_max_iters too large");
   SorArgs a;
+  memset(&a, 0, sizeof(a));
   a.coef = coef.p;
   a.b = b.p;
   a.x = x.p;
@@ -755,24 +772,52 @@ SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, c
   a.W = W;
   a.P = b.P;
   a.ps = ps;
-  a.nb = g.nblocks;
-  a.part = c->d_partials;
+  a.nstrips = nstrips;
+  a.stride = W + 64;
+  a.ticket = c->d_sor_sync;
+  a.prog = (int *)(c->d_sor_sync + 64);
+  a.fail = (int *)(c->d_sor_sync + 32);
   a.st = c->d_state;
   a.omega = (float)P->sor_omega;
-  a.tol = (float)P->sor_tol;
+  a.tol = P->sor_tol;
   a.maxiter = P->sor_max_iters;
-  launch(c, "sor_init", k_sor_init, g.grid, g.block, 0, a);
+  HIPCHK(hipMemsetAsync(c->d_sor_sync, 0, OF_SOR_SYNC_BYTES, c->stream));
+  launch(c, "sor_init", k_sor_init, dim3(std::min(1024, (H * b.P + 63) / 64)), dim3(64), 0, a);
+  double *sor_part = c->d_partials + 10 * PCG_MAX_BLOCKS;  // 2 x [2 * nstrips][2]
+  auto args_k = [&](int k) {
+    SorArgs ak = a;
+    ak.part_rd = sor_part + (size_t)((k + 1) & 1) * 2 * PCG_MAX_BLOCKS;
+    ak.part_wr = sor_part + (size_t)(k & 1) * 2 * PCG_MAX_BLOCKS;
+    return ak;
+  };
   int &hint = iter_hint(c, H, W, solver);
   const int enq = run_chunked(c, a.maxiter, hint > 0 ? std::max(16, hint * 3 / 4) : 16, 64, [&](int k) {
-    launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 0, k);
-    launch(c, "sor_sweep", k_sor_sweep, g.grid, g.block, 0, a, 1, k);
+    launch(c, "sor_sweep", k_sor_lex, dim3(2 * nstrips), dim3(64), OF_SOR_SHM, args_k(k), k);
   });
-  launch(c, "sor_final", k_sor_final, dim3(1), dim3(OF_BX, OF_BY), 0, a, enq);
+  launch(c, "sor_final", k_sor_final, dim3(1), dim3(64), 0, args_k(enq), enq);
   HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_norm, a.fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  const PcgState &s = c->h_state[0];
-  hint = s.iter;
-  return {s.iter, s.done, 0.0};
+  REQUIRE(*(const int *)c->h_norm == 0, OF_EHIP, "SOR strip hand-off timed out");
+  const PcgState &st = c->h_state[0];
+  hint = st.iter;
+  return {st.iter, st.done, st.xnorm2 > 0 ? std::sqrt(st.rr / st.xnorm2) : 0.0};
+}
+
+// _solve_linear_system; with the solve log on, followed by the fp64 true
+// residual of the final x (diagnostic, off by default)
+SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+  const SolveResult r = solve_impl(c, P, coef, b, x);
+  if (c->slog && c->slog_rec.size() < OF_SLOG_MAX) {
+    const int idx = (int)c->slog_rec.size();
+    Grid2 g = grid2(b.H, b.W, PCG_MAX_BLOCKS);
+    launch(c, "resid", k_resid_part, g.grid, g.block, 0, (const float *)coef.p, coef.ps(), (const float2 *)b.p,
+           (const float2 *)x.p, b.H, b.W, b.P, c->d_rpart);
+    launch(c, "resid", k_resid_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_rpart, g.nblocks,
+           c->d_rlog + 2 * idx);
+    c->slog_rec.push_back({b.H, b.W, P->solver, r.slot, r.iters, r.done, r.rel});
+  }
+  return r;
 }
 
 void note_solve_now(of_stats *st, const SolveResult &r) {
@@ -792,6 +837,14 @@ SolveResult resolved(of_ctx *c, int slot) {
 // statistics of the CG solves since the last stream synchronisation (call
 // only after one)
 void drain_solves(of_ctx *c) {
+  for (auto &l : c->slog_rec)
+    if (l.slot >= 0) {
+      const SolveResult r = resolved(c, l.slot);
+      l.iters = r.iters;
+      l.done = r.done;
+      l.est = r.rel;
+      l.slot = -1;
+    }
   for (const auto &p : c->pend) {
     const SolveResult r = resolved(c, p.slot);
     note_solve_now(p.st, r);
@@ -1236,7 +1289,11 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipHostGetDevicePointer((void **)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_state[1], hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 8 * PCG_MAX_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 16 * PCG_MAX_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_sor_sync, OF_SOR_SYNC_BYTES));
+    HIPCHK(hipMalloc(&c->d_rpart, sizeof(double) * 2 * PCG_MAX_BLOCKS));
+    HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 2 * OF_SLOG_MAX));
+    HIPCHK(hipFuncSetAttribute((const void *)k_sor_lex, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
     HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));
@@ -1271,6 +1328,9 @@ int of_ctx_destroy(of_ctx *c) {
   if (c->h_flag) hipHostFree(c->h_flag);
   if (c->h_ring) hipHostFree(c->h_ring);
   hipFree(c->d_partials);
+  hipFree(c->d_sor_sync);
+  hipFree(c->d_rpart);
+  hipFree(c->d_rlog);
   hipFree(c->d_mm);
   hipFree(c->d_norm);
   hipHostFree(c->h_norm);
@@ -1312,6 +1372,57 @@ int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t 
   }
   *n = k;
   return OF_OK;
+}
+
+int of_set_solve_log(of_ctx *c, int enable) {
+  if (!c) return OF_EINVAL;
+  c->slog = enable ? 1 : 0;
+  c->slog_rec.clear();
+  return OF_OK;
+}
+
+int of_solve_log(of_ctx *c, int max, of_solve_record *out, int *n) {
+  API_BEGIN(c)
+  REQUIRE(n && (out || max <= 0), OF_EINVAL, "bad arguments");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  drain_solves(c);
+  const int m = (int)c->slog_rec.size();
+  *n = m;
+  const int k = std::min(m, max);
+  if (k > 0) {
+    std::vector<double> h(2 * (size_t)k);
+    HIPCHK(hipMemcpy(h.data(), c->d_rlog, sizeof(double) * 2 * k, hipMemcpyDeviceToHost));
+    for (int e = 0; e < k; ++e) {
+      const auto &l = c->slog_rec[e];
+      of_solve_record &o = out[e];
+      memset(&o, 0, sizeof(o));
+      o.h = l.h;
+      o.w = l.w;
+      o.solver = l.solver;
+      o.iters = l.iters;
+      o.done = l.done;
+      o.true_rel = h[2 * e + 1] > 0 ? std::sqrt(h[2 * e] / h[2 * e + 1]) : 0.0;
+      o.est_rel = l.est;
+    }
+  }
+  API_END(c)
+}
+
+int of_solver_geometry(int H, int W, int solver, of_cg_geometry *out) {
+  if (!out || solver < 0 || solver > 2) return OF_EINVAL;
+  memset(out, 0, sizeof(*out));
+  if (solver == OF_SOLVER_SOR) {
+    if (H < 1 || W < 1) return OF_EINVAL;
+    const int ns = (H + 63) / 64;
+    out->grid_x = 2 * ns;
+    out->grid_y = 1;
+    out->rows = 64;
+    out->bands = ns;
+    out->blocks = 2 * ns;
+    out->strip_cols = W;
+    return ns <= SOR_MAXS ? OF_OK : OF_ENOTSUP;
+  }
+  return cg_geometry(H, W, solver == OF_SOLVER_BACKSLASH, out);
 }
 
 int of_estimate_flow(of_ctx *c, of_params *P, const float *im1, const float *im2, int H, int W, int C,
@@ -1446,11 +1557,10 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       c->lanes.push_back(l);
 
     }
-    // big-phase token threshold in pixels (OF_BIG_PX overrides; 0 = off).
-    // 8 1080p pairs, 2 lanes: 22.5 pairs/s with the token in three runs
-    // (16-18 without; 20.5 with one lane) -- two lanes' fine-level CG
-    // kernels, one 128-KB-LDS block per CU each, otherwise stall each other
-    static const double big_px = getenv("OF_BIG_PX") ? atof(getenv("OF_BIG_PX")) : (double)(1 << 20);
+    // big-phase token threshold in pixels.  8 1080p pairs, 2 lanes: 22.5
+    // pairs/s with the token in three runs (16-18 without; 20.5 with one
+    // lane) -- two lanes' fine-level CG kernels otherwise stall each other
+    const double big_px = OF_BIG_PX;
     std::vector<std::thread> th;
     std::vector<OfError> errs(lanes, OfError{OF_OK, ""});
     for (int li = 0; li < lanes; ++li) {

@@ -81,12 +81,17 @@ struct PcgArgs {
   int H, W, P;
   size_t ps;
   int nb;  // blocks of this grid (== blocks of every launch of the solve)
-  double *part;  // [5][PCG_MAX_BLOCKS] partial sums (layout per kernel pair)
+  // per-block partial sums [5][PCG_MAX_BLOCKS], ping-ponged by iteration
+  // parity: launch k reads launch k-1's (part_rd) and writes its own
+  // (part_wr).  One buffer would race: a block that starts after another
+  // block of the same grid has finished would read a mix of both launches.
+  const double *part_rd;
+  double *part_wr;
   PcgState *st;
   CgFlag *hflag;  // mapped host memory (may be null)
   double rtol;
   int maxiter;
-  float poly[4];  // k_cgp: M^-1 = (poly[0] + poly[1] B + poly[2] B^2 + poly[3] B^3) D^-1
+  float poly[4];  // k_cgs: M^-1 = (poly[0] + poly[1] B + poly[2] B^2 + poly[3] B^3) D^-1
 };
 
 // the shared prologue: returns 1 when the solve is finished (state written)
@@ -94,7 +99,7 @@ __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds
   __shared__ int s_exit;
   __shared__ float s_ab[2];
   double S[5];
-  prologue_sum<5>(S, g.part, g.nb, lds);  // of K_{k-1}: pq, qz, qMq, rz, rr
+  prologue_sum<5>(S, g.part_rd, g.nb, lds);  // of K_{k-1}: pq, qz, qMq, rz, rr
   if (threadIdx.x == 0 && threadIdx.y == 0) {
     const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
     const double rn = sqrt(S[4]);
@@ -243,7 +248,7 @@ __device__ __forceinline__ cg_f4 cg_minv(const CgInv &m, cg_f4 r) {
 }
 __device__ __forceinline__ float cg_dot(cg_f4 a, cg_f4 b) { return a.x * b.x + a.y * b.y + (a.z * b.z + a.w * b.w); }
 
-// Launch prologue of k_cg / k_cgn: fixed-order sum of the previous launch's
+// Launch prologue of k_cg / k_cgs: fixed-order sum of the previous launch's
 // per-block partials (pq, qz, qMq, rz, rr) -> alpha_{k-1}, rho_k (CG
 // recurrence), beta_k, scipy's convergence test; the lead block records the
 // state.  Returns true when this launch has nothing to do.
@@ -263,7 +268,7 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
       double s = 0.0;
-      for (int b = tid; b < g.nb; b += 256) s += g.part[(size_t)v * PCG_MAX_BLOCKS + b];
+      for (int b = tid; b < g.nb; b += 256) s += g.part_rd[(size_t)v * PCG_MAX_BLOCKS + b];
       S[v] = wave_sum(s);
     }
     if ((tid & 63) == 0)
@@ -437,219 +442,20 @@ __global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands)
       }
     }
   }
-  write_partials<5>(acc, g.part, lds);
+  write_partials<5>(acc, g.part_wr, lds);
 }
 
 // ---------------------------------------------------------------------------
-// k_cgn: the same fused, q-free CG iteration with the first-order Neumann
-// preconditioner of the 2x2 block-Jacobi splitting A = D - N:
-//   M^-1 = D^-1 + D^-1 N D^-1,   z = D^-1 (r + N y),  y = D^-1 r
-// (symmetric; positive definite since D + N is a signless graph Laplacian
-// plus the PSD data blocks).  On Classic+NL stage-2 systems it halves the
-// CG iteration count of block Jacobi (measured: 435 -> 217 on RubberWhale,
-// 277 -> 138 on a 540x960 synthetic pair) for one more neighbour exchange.
-// The recurrence term q.M^-1 q = q.y_q + 2 sum_edges w y_q,i y_q,j (y_q =
-// D^-1 q) is accumulated edge by edge: horizontal edges by their left pixel,
-// vertical edges by their lower pixel.
-//
-// Horizontal dependency depth is 3 columns (q <- p <- z <- y <- r <- A
-// p_old), so a strip carries two halo lanes per side: PCG_SWN = 120 output
-// columns, lanes 2..61.
-//
-// Pipeline (step t): A) r, y of row t+1 (needs p_old rows t..t+2);
-// B) z, p of row t (y rows t-1..t+1), x of row t; C) q = A p, y_q of row
-// t-1 (p rows t-2..t), then stores and dot products when t-1 is an output
-// row.  Rows live in 4-slot register rings, the loop is unrolled by 4.
-// The band is entered at t = r0 - 4 so that y_q of row r0 - 1 exists.
-
-#define PCG_SWN 120
-
-// sum of the neighbour terms N f of the middle row (no diagonal)
-__device__ __forceinline__ cg_f4 cg_nsum(cg_f4 up, cg_f4 mid, cg_f4 dn, const CgCoef &c, cg_f2 wuu, cg_f2 wuv) {
-  const float Lu = cg_from_left(mid.z), Lv = cg_from_left(mid.w);
-  const float Ru = cg_from_right(mid.x), Rv = cg_from_right(mid.y);
-  cg_f4 o;
-  o.x = c.wlu * Lu + c.wxu.x * mid.z + wuu.x * up.x + c.wyu.x * dn.x;
-  o.y = c.wlv * Lv + c.wxv.x * mid.w + wuv.x * up.y + c.wyv.x * dn.y;
-  o.z = c.wxu.x * mid.x + c.wxu.y * Ru + wuu.y * up.z + c.wyu.y * dn.z;
-  o.w = c.wxv.x * mid.y + c.wxv.y * Rv + wuv.y * up.w + c.wyv.y * dn.w;
-  return o;
-}
-__device__ __forceinline__ cg_f4 cg_diag(const CgCoef &c, cg_f4 f) {
-  cg_f4 o;
-  o.x = c.a.x * f.x + c.c.x * f.y;
-  o.y = c.c.x * f.x + c.d.x * f.y;
-  o.z = c.a.y * f.z + c.c.y * f.w;
-  o.w = c.c.y * f.z + c.d.y * f.w;
-  return o;
-}
-
-template <bool FIRST, bool ODD>
-__global__ __launch_bounds__(256) void k_cgn(PcgArgs g, int k, int R, int nbands) {
-  __shared__ double lds[64];
-  const int H = g.H, W = g.W;
-  const unsigned rowb4 = (unsigned)g.P * 4u, rowb8 = (unsigned)g.P * 8u;
-  const size_t vbytes = (size_t)H * g.P * 8;
-  const __amdgpu_buffer_rsrc_t rc = cg_rsrc(g.coef, g.ps * 7 * 4);
-  const __amdgpu_buffer_rsrc_t rin = cg_rsrc(FIRST ? g.b : g.r_in, vbytes);
-  const __amdgpu_buffer_rsrc_t rpo = cg_rsrc(g.p_old, vbytes);
-  const __amdgpu_buffer_rsrc_t rx = cg_rsrc(g.x, vbytes);
-  const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
-  const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
-  const unsigned ps4 = (unsigned)(g.ps * 4);
-  // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
-  const int lane = threadIdx.x, band = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.y);
-  const int jc = blockIdx.x * PCG_SWN - 4 + 2 * lane;
-  const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
-  const bool out_lane = lane >= 2 && lane <= 61;
-  const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
-  const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
-  const bool live = band < nbands;
-  const int r0 = band * R, r1 = min(r0 + R, H);
-  auto o4 = [&](int t) { return (unsigned)t < (unsigned)H ? off4 + (unsigned)t * rowb4 : CG_OOB; };
-  auto o8 = [&](int t) { return (unsigned)t < (unsigned)H ? off8 + (unsigned)t * rowb8 : CG_OOB; };
-  auto load_coef = [&](int t, CgCoef &c) {
-    const unsigned v = o4(t);
-    c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
-    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
-    c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
-    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
-    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
-    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
-    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
-  };
-  auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
-  auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
-  auto load_x = [&](int t) {
-    return (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
-  };
-  const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const cg_f2 zero2 = {0.f, 0.f};
-
-  // rings: slot of row (t0 + u + d) is (u + d) & 3, t0 = r0 - 4 + 4n
-  CgCoef C[4];   // coefficients (+ left weights), rows t-1 .. t+1, t+2 loading
-  CgInv MI[4];   // D^-1 of the same rows
-  cg_f2 WYU[2], WYV[2];  // vertical weights of row t-2
-  cg_f4 PO[4];   // p_old rows t .. t+2, t+3 loading
-  cg_f4 RI[2];   // r_in rows t+1, t+2 loading
-  cg_f4 XI[2];   // x rows t, t+1 loading
-  if (live) {
-    const int t = r0 - 4;
-    C[0].wxu = C[0].wxv = C[0].a = C[0].c = C[0].d = zero2;
-    C[0].wlu = C[0].wlv = 0.f;
-    {  // row t: only its vertical weights feed stage A of row t+1
-      const unsigned v = o4(t);
-      C[0].wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
-      C[0].wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
-    }
-    load_coef(t + 1, C[1]);
-    PO[0] = load_po(t);
-    PO[1] = load_po(t + 1);
-    PO[2] = load_po(t + 2);
-    RI[1] = load_rin(t + 1);
-    XI[0] = zero4;
-  }
-  float alpha = 0.f, beta = 0.f;
-  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
-
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (live) {
-    cg_f4 RR[4] = {zero4, zero4, zero4, zero4};  // r rows t-1 .. t+1
-    cg_f4 YY[4] = {zero4, zero4, zero4, zero4};  // y = D^-1 r, rows t-1 .. t+1
-    cg_f4 PP[4] = {zero4, zero4, zero4, zero4};  // p rows t-2 .. t
-    cg_f4 ZZ[2] = {zero4, zero4};                // z rows t-1, t
-    cg_f4 YQ[2] = {zero4, zero4};                // y_q rows t-2, t-1
-    WYU[0] = WYU[1] = WYV[0] = WYV[1] = zero2;
-    C[2] = C[0];
-    C[3] = C[0];
-    MI[0] = MI[2] = MI[3] = cg_inv<true>(C[0]);
-    const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;
-    for (int t0 = r0 - 4; t0 <= r1; t0 += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int t = t0 + u;
-        if (t > r1) break;
-        CgCoef &cm1 = C[(u + 3) & 3], &c0 = C[u & 3], &cp1 = C[(u + 1) & 3], &cp2 = C[(u + 2) & 3];
-        // keep the vertical weights of row t-2, then prefetch row t+2
-        WYU[u & 1] = cp2.wyu;
-        WYV[u & 1] = cp2.wyv;
-        load_coef(t + 2, cp2);
-        RI[u & 1] = load_rin(t + 2);
-        PO[(u + 3) & 3] = load_po(t + 3);
-        XI[(u + 1) & 1] = load_x(t + 1);
-        // A) row t+1: r = r_in - alpha A p_old, y = D^-1 r
-        cp1.wlu = cg_from_left(cp1.wxu.y);
-        cp1.wlv = cg_from_left(cp1.wxv.y);
-        MI[(u + 1) & 3] = cg_inv<true>(cp1);
-        cg_f4 r = RI[(u + 1) & 1];
-        if (!FIRST)
-          r -= alpha * (cg_diag(cp1, PO[(u + 1) & 3]) -
-                        cg_nsum(PO[u & 3], PO[(u + 1) & 3], PO[(u + 2) & 3], cp1, c0.wyu, c0.wyv));
-        {
-          const bool rv = (unsigned)(t + 1) < (unsigned)H;
-          if (!(rv && ok0)) { r.x = 0.f; r.y = 0.f; }
-          if (!(rv && ok1)) { r.z = 0.f; r.w = 0.f; }
-        }
-        RR[(u + 1) & 3] = r;
-        YY[(u + 1) & 3] = cg_minv(MI[(u + 1) & 3], r);
-        // B) row t: z = D^-1 (r + N y), p = z + beta p_old, x += alpha p_old
-        const cg_f4 z = cg_minv(MI[u & 3], RR[u & 3] + cg_nsum(YY[(u + 3) & 3], YY[u & 3], YY[(u + 1) & 3], c0,
-                                                                cm1.wyu, cm1.wyv));
-        cg_f4 p = FIRST ? z : z + beta * PO[u & 3];
-        {
-          const bool rv = (unsigned)t < (unsigned)H;
-          if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
-          if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
-        }
-        PP[u & 3] = p;
-        ZZ[u & 1] = z;
-        if (t >= r0 && t < r1) cg_st4(rx, soff8 + (unsigned)t * rowb8, FIRST ? zero4 : XI[u & 1] + alpha * PO[u & 3]);
-        // C) row t-1: q = A p, y_q = D^-1 q; stores and dots for output rows
-        const int o = t - 1;
-        const cg_f4 pm1 = PP[(u + 3) & 3];
-        const CgCoef &cq = cm1;
-        const cg_f4 q = cg_diag(cq, pm1) - cg_nsum(PP[(u + 2) & 3], pm1, p, cq, WYU[u & 1], WYV[u & 1]);
-        const cg_f4 yq = cg_minv(MI[(u + 3) & 3], q);
-        if (o >= r0 && o < r1) {
-          const cg_f4 rm1 = RR[(u + 3) & 3], zm1 = ZZ[(u + 1) & 1], yqu = YQ[(u + 1) & 1];
-          const unsigned so = soff8 + (unsigned)o * rowb8;
-          cg_st4(rro, so, rm1);
-          cg_st4(rpn, so, pm1);
-          // edge terms of q.M^-1 q: right edges of the lane's pixels, edges
-          // to the row above
-          const float yRu = cg_from_right(yq.x), yRv = cg_from_right(yq.y);
-          const float e0 = cq.wxu.x * yq.x * yq.z + cq.wxv.x * yq.y * yq.w + WYU[u & 1].x * yqu.x * yq.x +
-                           WYV[u & 1].x * yqu.y * yq.y;
-          const float e1 = cq.wxu.y * yq.z * yRu + cq.wxv.y * yq.w * yRv + WYU[u & 1].y * yqu.z * yq.z +
-                           WYV[u & 1].y * yqu.w * yq.w;
-          cg_f4 qm = q, rm = rm1;
-          float em = 0.f;
-          if (dm0) em += e0;
-          else { qm.x = 0.f; qm.y = 0.f; rm.x = 0.f; rm.y = 0.f; }
-          if (dm1) em += e1;
-          else { qm.z = 0.f; qm.w = 0.f; rm.z = 0.f; rm.w = 0.f; }
-          acc[0] += (double)cg_dot(pm1, qm);
-          acc[1] += (double)cg_dot(qm, zm1);
-          acc[2] += (double)(cg_dot(qm, yq) + 2.0f * em);
-          acc[3] += (double)cg_dot(rm, zm1);
-          acc[4] += (double)cg_dot(rm, rm1);
-        }
-        YQ[u & 1] = yq;
-      }
-    }
-  }
-  write_partials<5>(acc, g.part, lds);
-}
-
-// ---------------------------------------------------------------------------
-// k_cgp: the fused, q-free CG iteration with a degree-3 polynomial
-// preconditioner in the 2x2 block-Jacobi splitting A = D - N, B = D^-1 N:
+// The 'backslash' surrogate iteration (k_cgs below): the fused, q-free CG
+// iteration with a degree-3 polynomial preconditioner in the 2x2
+// block-Jacobi splitting A = D - N, B = D^-1 N:
 //   M^-1 = (c0 + c1 B + c2 B^2 + c3 B^3) D^-1,
 // the Chebyshev polynomial that minimises max |1 - X p(X)| for the spectrum
 // of X = D^-1 A = I - B on [0.04, 2] (host: cheb_poly; 2 bounds the
 // spectrum because D + N is positive semidefinite).  p > 0 there, so M is
 // SPD.  Measured on Classic+NL stage-2 systems (RubberWhale, 1e-6 relative
-// residual): 0.54x the iterations of the first-order Neumann kernel k_cgn.
+// residual): 0.54x the iterations of a first-order Neumann preconditioner,
+// 0.27x of block Jacobi.
 //
 // z = M^-1 r by Horner, one neighbour exchange per stage:
 //   y = D^-1 r,  g2 = c2 y + c3 D^-1 N y,  g1 = c1 y + D^-1 N g2,
@@ -657,20 +463,12 @@ __global__ __launch_bounds__(256) void k_cgn(PcgArgs g, int k, int R, int nbands
 // The rho recurrence needs q.M^-1 q = sum_i c_i T_i with y_q = D^-1 q,
 // v1 = D^-1 N y_q:  T0 = y_q.q, T1 = y_q.N y_q, T2 = v1.N y_q (= v1.D v1),
 // T3 = v1.N v1 (each edge counted once, by its right / lower pixel).
-//
-// Pipeline (step n): A) r, y of row n-1; B) g2 of row n-2; C) g1 of row
-// n-3; D) z, p, x of row n-4; E) q, y_q of row n-5; F) v1 and the T terms
-// of row n-6.  Seven stencil stages deep, so a strip carries four halo
-// lanes per side (PCG_SWP = 112 output columns, lanes 4..59) and a band is
-// entered at row r0 - 7 and left at r1 + 5.
-// Arithmetic is on (u, v) pairs of one pixel (packed fp32: v_pk_fma_f32).
-// Each row's coefficients are staged once into a per-wave LDS ring (8 rows;
-// per pixel the (u, v) weight pairs of the edges right and below and D^-1
-// as (ia, ic), (ic, id); 32 KB per wave) that every stage reads; D itself
-// is re-formed from D^-1 where a stage needs it.  Vectors live in register
-// rings indexed by (row - (r0 - 7)); the loop is unrolled by eight so every
-// ring index is a compile-time constant.  Global loads run two steps ahead
-// (coefficients of row n+3, p_old of row n+2), r_in and x one step.
+// Seven stencil stages deep, so a strip carries four halo lanes per side
+// (PCG_SWP = 112 output columns, lanes 4..59).  Arithmetic is on (u, v)
+// pairs of one pixel (packed fp32: v_pk_fma_f32).  Each row's coefficients
+// are staged once into an LDS ring of records (per pixel the (u, v) weight
+// pairs of the edges right and below and D^-1 as (ia, ic), (ic, id)) that
+// every stage reads; D itself is re-formed from D^-1 where a stage needs it.
 #define PCG_SWP 112
 #define CG_ROW_OOB 0x40000000u
 
@@ -717,262 +515,16 @@ __device__ __forceinline__ cg_f4 cgr_diag(const CgRec &m, cg_f4 f) {
   return cg_cat(o[0], o[1]);
 }
 
-template <bool FIRST, bool ODD>
-__global__ __launch_bounds__(256) void k_cgp(PcgArgs g, int k, int R, int nbands) {
-  __shared__ double lds[64];
-  __shared__ float4 ring[4][8][4][64];  // [wave][row slot][record quarter][lane]
-  const int H = g.H, W = g.W;
-  const unsigned rowb4 = (unsigned)g.P * 4u, rowb8 = (unsigned)g.P * 8u;
-  const size_t vbytes = (size_t)H * g.P * 8;
-  const __amdgpu_buffer_rsrc_t rc = cg_rsrc(g.coef, g.ps * 7 * 4);
-  const __amdgpu_buffer_rsrc_t rin = cg_rsrc(FIRST ? g.b : g.r_in, vbytes);
-  const __amdgpu_buffer_rsrc_t rpo = cg_rsrc(g.p_old, vbytes);
-  const __amdgpu_buffer_rsrc_t rx = cg_rsrc(g.x, vbytes);
-  const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
-  const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
-  const unsigned ps4 = (unsigned)(g.ps * 4);
-  // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
-  const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = blockIdx.y * 4 + wid;
-  const int jc = blockIdx.x * PCG_SWP - 8 + 2 * lane;
-  const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
-  const bool out_lane = lane >= 4 && lane <= 59;
-  const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
-  const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
-  const bool live = band < nbands;
-  const int r0 = band * R, r1 = min(r0 + R, H);
-  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
-  // row part of an offset: wave-uniform (SALU); rows outside [0, H) get
-  // CG_ROW_OOB, which keeps every lane's sum out of range without wrapping
-  // (lane parts are < 2^24 or CG_OOB; buffers < CG_ROW_OOB bytes, host-checked)
-  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb4 : CG_ROW_OOB); };
-  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb8 : CG_ROW_OOB); };
-  auto load_raw = [&](int t, CgRaw &c) {
-    const unsigned v = o4(t);
-    c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
-    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
-    c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
-    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
-    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
-    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
-    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
-  };
-  // raw row -> LDS ring slot (per pixel: wx, wy pairs; D^-1 columns)
-  auto put_rec = [&](int slot, const CgRaw &c) {
-    CgCoef cc;
-    cc.a = c.a;
-    cc.c = c.c;
-    cc.d = c.d;
-    const CgInv mi = cg_inv<true>(cc);
-    float4 *q = &ring[wid][slot][0][lane];
-    q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
-    q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
-    q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
-    q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
-  };
-  auto get_rec = [&](int slot) {
-    const float4 *q = &ring[wid][slot][0][lane];
-    const float4 a = q[0], b = q[64], c = q[128], d = q[192];
-    CgRec r;
-    r.wx[0] = cg_f2{a.x, a.y};
-    r.wy[0] = cg_f2{a.z, a.w};
-    r.wx[1] = cg_f2{b.x, b.y};
-    r.wy[1] = cg_f2{b.z, b.w};
-    r.ma[0] = cg_f2{c.x, c.y};
-    r.mb[0] = cg_f2{c.z, c.w};
-    r.ma[1] = cg_f2{d.x, d.y};
-    r.mb[1] = cg_f2{d.z, d.w};
-    return r;
-  };
-  auto get_wy = [&](int slot, cg_f2 (&wu)[2]) {  // vertical weight pairs only
-    const float2 *q = reinterpret_cast<const float2 *>(&ring[wid][slot][0][lane]);
-    const float2 a = q[1], b = q[129];
-    wu[0] = cg_f2{a.x, a.y};
-    wu[1] = cg_f2{b.x, b.y};
-  };
-  auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
-  auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
-  auto load_x = [&](int t) {
-    return (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
-  };
-  // dot products of output pixels only (select, not multiply: halo lanes
-  // may hold inf/nan)
-  const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;
-  auto mdot = [&](cg_f4 a, cg_f4 b) {
-    const cg_f2 p = cg_lo(a) * cg_lo(b), q = cg_hi(a) * cg_hi(b);
-    return (dm0 ? p.x + p.y : 0.f) + (dm1 ? q.x + q.y : 0.f);
-  };
-  const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const int ns = r0 - 7, ne = r1 + 5;
-
-  CgRaw SG[2];   // staged coefficient rows n+2, n+3
-  cg_f4 PO[8];   // p_old of rows n-4 .. n+2
-  cg_f4 RI[2];   // r_in of rows n-1, n
-  cg_f4 XI[2];   // x of rows n-4, n-3
-  if (live) {
-    // rows ns .. ns+2 (coefficients), ns, ns+1 (p_old), ns (r_in)
-    load_raw(ns, SG[0]);
-    PO[0] = load_po(ns);
-    PO[1] = load_po(ns + 1);
-    RI[0] = load_rin(ns);
-#pragma unroll
-    for (int s = 2; s < 8; ++s) PO[s] = zero4;
-    RI[1] = zero4;
-    XI[0] = XI[1] = zero4;
-  }
-  float alpha = 0.f, beta = 0.f;
-  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
-
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (live) {
-    {
-      // ring slot 0 <- row ns; slots 1..7 <- zero rows (read before written
-      // only by stages whose rows lie above the band's valid region)
-      put_rec(0, SG[0]);
-      CgRaw zr;
-      zr.wxu = zr.wyu = zr.wxv = zr.wyv = zr.a = zr.c = zr.d = cg_f2{0.f, 0.f};
-#pragma unroll
-      for (int s = 1; s < 8; ++s) put_rec(s, zr);
-      load_raw(ns + 1, SG[1]);
-      load_raw(ns + 2, SG[0]);
-    }
-    cg_f4 YR[4], G2[4], G1[4], PP[4], YQ[4], ZZ[2], V1[2];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) YR[s] = G2[s] = G1[s] = PP[s] = YQ[s] = zero4;
-    ZZ[0] = ZZ[1] = V1[0] = V1[1] = zero4;
-    for (int n0 = ns; n0 <= ne; n0 += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int n = n0 + u;
-        if (n > ne) break;
-        // ring slots: row n + d lives in PO / LDS slot (u + d) & 7, in the
-        // 4-rings at (u + d) & 3 and in the 2-rings at (u + d) & 1
-#define S8(d) ((u + (d) + 16) & 7)
-#define S4(d) ((u + (d) + 16) & 3)
-#define S2(d) ((u + (d) + 16) & 1)
-        // vertical weights of row n-7 (its slot is about to take row n+1)
-        cg_f2 wy7[2];
-        get_wy(S8(-7), wy7);
-        put_rec(S8(1), SG[S2(1)]);
-        load_raw(n + 3, SG[S2(1)]);
-        PO[S8(2)] = load_po(n + 2);
-        RI[S2(0)] = load_rin(n);
-        XI[S2(-3)] = load_x(n - 3);
-        // LDS records are read one stage ahead of their use (the ds_read
-        // latency overlaps the previous stage's arithmetic)
-        CgRec qn = get_rec(S8(-1));
-        cg_f2 wn[2];
-        get_wy(S8(-2), wn);
-        // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
-        {
-          const CgRec q1 = qn;
-          cg_f2 wu[2] = {wn[0], wn[1]};
-          qn = get_rec(S8(-2));
-          get_wy(S8(-3), wn);
-          cg_f4 r = RI[S2(-1)];
-          if (!FIRST) r -= alpha * (cgr_diag(q1, PO[S8(-1)]) - cgr_nsum(PO[S8(-2)], PO[S8(-1)], PO[S8(0)], q1, wu));
-          const cg_f4 y = cgr_minv(q1, r);
-          YR[S4(-1)] = y;
-          const int o = n - 1;
-          if (o >= r0 && o < r1) {
-            cg_st4(rro, soff8 + (unsigned)o * rowb8, r);
-            acc[4] += (double)mdot(r, r);
-            acc[3] += (double)(c0 * mdot(r, y));
-          }
-        }
-        // B) row n-2: g2 = c2 y + c3 D^-1 N y
-        {
-          const CgRec q2 = qn;
-          cg_f2 wu[2] = {wn[0], wn[1]};
-          qn = get_rec(S8(-3));
-          get_wy(S8(-4), wn);
-          const cg_f4 ny = cgr_nsum(YR[S4(-3)], YR[S4(-2)], YR[S4(-1)], q2, wu);
-          G2[S4(-2)] = c2 * YR[S4(-2)] + c3 * cgr_minv(q2, ny);
-        }
-        // C) row n-3: g1 = c1 y + D^-1 N g2
-        {
-          const CgRec q3 = qn;
-          cg_f2 wu[2] = {wn[0], wn[1]};
-          qn = get_rec(S8(-4));
-          get_wy(S8(-5), wn);
-          const cg_f4 ng = cgr_nsum(G2[S4(-4)], G2[S4(-3)], G2[S4(-2)], q3, wu);
-          G1[S4(-3)] = c1 * YR[S4(-3)] + cgr_minv(q3, ng);
-        }
-        // D) row n-4: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
-        {
-          const CgRec q4 = qn;
-          cg_f2 wu[2] = {wn[0], wn[1]};
-          qn = get_rec(S8(-5));
-          get_wy(S8(-6), wn);
-          const cg_f4 ng = cgr_nsum(G1[S4(-5)], G1[S4(-4)], G1[S4(-3)], q4, wu);
-          const cg_f4 yr = YR[S4(-4)];
-          const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
-          cg_f4 p = FIRST ? z : z + beta * PO[S8(-4)];
-          const int o = n - 4;
-          const bool rv = (unsigned)o < (unsigned)H;
-          if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
-          if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
-          PP[S4(-4)] = p;
-          ZZ[S2(-4)] = z;
-          if (o >= r0 && o < r1) {
-            const unsigned so = soff8 + (unsigned)o * rowb8;
-            cg_st4(rpn, so, p);
-            cg_st4(rx, so, FIRST ? zero4 : XI[S2(-4)] + alpha * PO[S8(-4)]);
-            acc[3] += (double)mdot(yr, ng);
-          }
-        }
-        // E) row n-5: q = A p, y_q = D^-1 q
-        {
-          const CgRec q5 = qn;
-          cg_f2 wu[2] = {wn[0], wn[1]};
-          qn = get_rec(S8(-6));
-          const cg_f4 pm = PP[S4(-5)];
-          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[S4(-6)], pm, PP[S4(-4)], q5, wu);
-          const cg_f4 yq = cgr_minv(q5, q);
-          YQ[S4(-5)] = yq;
-          const int o = n - 5;
-          if (o >= r0 && o < r1) {
-            acc[0] += (double)mdot(pm, q);
-            acc[1] += (double)mdot(q, ZZ[S2(-5)]);
-            acc[2] += (double)(c0 * mdot(q, yq));
-          }
-        }
-        // F) row n-6: N y_q, v1 = D^-1 N y_q, T1..T3
-        {
-          const CgRec q6 = qn;
-          const cg_f4 yq = YQ[S4(-6)];
-          const cg_f4 ny = cgr_nsum(YQ[S4(-7)], yq, YQ[S4(-5)], q6, wy7);
-          const cg_f4 v1 = cgr_minv(q6, ny);
-          const cg_f4 vu = V1[S2(-7)];
-          V1[S2(-6)] = v1;
-          const int o = n - 6;
-          if (o >= r0 && o < r1) {
-            // edges to the left and above, counted by this (right / lower)
-            // pixel: N v1 restricted to those edges
-            const cg_f2 v0 = cg_lo(v1), vv1 = cg_hi(v1);
-            const cg_f2 h0 = cg_left2(q6.wx[1]) * cg_left2(vv1) + wy7[0] * cg_lo(vu);
-            const cg_f2 h1 = q6.wx[0] * v0 + wy7[1] * cg_hi(vu);
-            const cg_f4 t = (c1 * yq + c2 * v1) * ny + (2.0f * c3) * v1 * cg_cat(h0, h1);
-            acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
-          }
-        }
-#undef S8
-#undef S4
-#undef S2
-      }
-    }
-  }
-  write_partials<5>(acc, g.part, lds);
-}
 
 // ---------------------------------------------------------------------------
 // k_cg_small: a whole CG solve in ONE workgroup, for levels of at most
-// CG_SMALL_PX pixels.  At the coarse pyramid levels a fused k_cgp launch is
+// CG_SMALL_PX pixels.  At the coarse pyramid levels a fused k_cgs launch is
 // latency-bound (~23 us however few rows: its 7-stage row pipeline is walked
 // by one wave per band), and a solve is one launch per iteration; here the
 // whole solve is one launch.  Textbook preconditioned CG with the control
 // flow of scipy.sparse.linalg.cg (base.py:116-136): x0 = 0, stop when
 // ||r|| < rtol ||b|| before an iteration, at most maxiter iterations.
-// Preconditioner as in the fused kernels: DEG 3 = k_cgp's Chebyshev
+// Preconditioner as in the fused kernels: DEG 3 = k_cgs's Chebyshev
 // polynomial in the 2x2 block-Jacobi splitting A = D - N (Horner, three
 // neighbour sums), DEG 0 = D^-1 (2x2 blocks if BLOCK, else scipy's scalar
 // Jacobi).  Vectors live in global memory (L2-resident at these sizes);
@@ -1161,19 +713,18 @@ template __global__ void k_cg_small<0, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, false>(CgSmallArgs);
 
 // ---------------------------------------------------------------------------
-// k_cgs: k_cgp's iteration (same preconditioner, same rho recurrence, same
-// per-element arithmetic) with its pipeline stages split over the 4 waves of
-// a block, which all work on ONE band:
+// k_cgs: the degree-3 iteration above with its pipeline stages split over
+// the 4 waves of a block, which all work on ONE band:
 //   wave 0: loads, coefficient records -> LDS ring, A) r, y of row n-1
 //   wave 1: B) g2 of row n-3, C) g1 of row n-4
 //   wave 2: D) z, p, x of row n-6, E) q, y_q of row n-7
 //   wave 3: F) v1 and the T terms of row n-9
 // with one block barrier per row step; rows cross waves through small LDS
 // rings (y, g1, y_q; records in a 12-row ring), a wave's own rows stay in
-// registers.  k_cgp gives each wave its own band and the whole pipeline, so
-// a band of R rows costs R + 12 steps of all 6 stages per wave and its
-// 32-KB record ring allows one wave per SIMD (R = 20 at 1080p: 1.6x the rows
-// read); here 64 KB of LDS per block allow 2 blocks per CU (R = 39 at
+// registers.  (Round 1's k_cgp gave each wave its own band and the whole
+// pipeline: a band of R rows cost R + 12 steps of all 6 stages per wave and
+// its 32-KB record ring allowed one wave per SIMD, R = 20 at 1080p, 1.6x the
+// rows read.)  Here 64 KB of LDS per block allow 2 blocks per CU (R = 39 at
 // 1080p, 1.36x) and a step costs only the heaviest wave's share.
 // Stage lags follow from one barrier per step: a stage reads rows of another
 // wave produced at earlier steps; the band is walked for n in
@@ -1440,7 +991,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #undef R2
 #undef CGS_STEPS
   }
-  write_partials<5>(acc, g.part, lds);
+  write_partials<5>(acc, g.part_wr, lds);
 }
 
 // after the last enqueued iteration: apply the convergence test to the last
@@ -1457,90 +1008,260 @@ __global__ __launch_bounds__(256) void k_pcg_check(PcgArgs g, int k) {
 }
 
 // ---------------------------------------------------------------------------
-// red-black block SOR (the GPU form of base.py:138-172): pixels of one colour
-// are independent; each solves its own 2x2 (u, v) block against the current
-// neighbours and relaxes with omega.  Convergence ||x - x_old|| < tol ||x||
-// per full sweep is evaluated in the prologue of the next red sweep.
+// Lexicographic SOR, exactly the reference's sweep order (base.py:138-172).
+// The reference walks the 2N rows of the CSR matrix in order: all u unknowns
+// in Fortran order (index i + j*H: down each column, columns left to right),
+// then all v unknowns in the same order, each row relaxed in place
+//   x_r <- (1 - w) x_r + w (b_r - sum_{c != r} A_rc x_c) / A_rr
+// (rows with |A_rr| < 1e-15 skipped), and stops after the first sweep with
+// ||x - x_old|| < tol ||x|| (at most max_iters sweeps, x0 = 0).
+//
+// With A = D - N (2x2 blocks D = [[a, c], [c, d]], N = edge weights), row
+// (i, j) of the u half reads u(i-1, j), u(i, j-1) already relaxed this
+// sweep, u(i+1, j), u(i, j+1) not yet, and v(i, j) of the previous sweep;
+// the v half reads v neighbours the same way and the NEW u(i, j).  So a
+// sweep is a Gauss-Seidel pass over the u plane followed by one over the v
+// plane, and the update of (i, j) depends only on (i-1, j) and (i, j-1):
+// every anti-diagonal i + j = const may be relaxed at once without changing
+// a single operand.  The GPU form keeps the reference's iterate exactly
+// (up to fp32 rounding):
+//   - a launch is one sweep; each 64-thread block (one wave) owns a strip of
+//     64 rows of ONE half (u or v); lane l = row i0 + l walks its own row,
+//     and at step t relaxes column t - l, so the wave's active points form an
+//     anti-diagonal: the up neighbour (relaxed by lane l-1 at step t-1) and
+//     the down neighbour (lane l+1's not-yet-relaxed next point) arrive by
+//     DPP lane shifts, left / right are the lane's own previous / next point;
+//   - strips hand rows to each other through global memory: strip s needs
+//     the relaxed last row of strip s-1 (same half), and the v strip s needs
+//     the relaxed u of its own rows; producers publish their completed step
+//     count every SOR_G steps (sc1 stores of x, s_waitcnt vmcnt(0), sc1 flag
+//     store) and consumers poll with sc1 loads and read x only with sc1 loads
+//     (MI355X_MICROARCH.md, hand-off table row 1: no L1 copy of x is ever
+//     used, so no acquire fence is needed);
+//   - blocks take their strip from a ticket counter in dependency order (u
+//     strips 0.., then v strips 0..), so a block only ever waits for blocks
+//     that hold lower tickets and are therefore already running: the launch
+//     cannot deadlock whatever the dispatch order or occupancy;
+//   - the stopping test of sweep k-1 runs in the prologue of launch k on the
+//     per-strip fp64 partials (fixed order, so every block agrees), ping-
+//     ponged by sweep parity.
+#define SOR_D 4    // prefetch distance in steps
+#define SOR_G 64   // steps between progress publications
+#define SOR_MAXS (PCG_MAX_BLOCKS / 2)
+
 struct SorArgs {
-  const float *coef;
+  const float *coef;  // 7 planes {wx_u, wy_u, wx_v, wy_v, a, c, d}, plane stride ps
   const float2 *b;
   float2 *x;
   int H, W, P;
   size_t ps;
-  int nb;
-  double *part;  // [2 colours][2 sums][PCG_MAX_BLOCKS]
+  int nstrips;          // strips per half; blocks per launch = 2 * nstrips
+  int stride;           // progress stamp of launch k = k * stride + steps done
+  unsigned *ticket;     // reset per solve
+  int *prog;            // [2][SOR_MAXS] progress stamps, reset per solve
+  int *fail;            // set when a hand-off wait gave up (reset per solve)
+  const double *part_rd;  // [2 * nstrips][2] (dn, xn) of the previous sweep
+  double *part_wr;
   PcgState *st;
-  float omega, tol;
+  float omega;
+  double tol;
   int maxiter;
 };
 
-__global__ __launch_bounds__(256) void k_sor_init(SorArgs a) {
-  OF_FOR_PIXELS(a.H, a.W) {
-    if (j < a.W) a.x[(size_t)i * a.P + j] = make_float2(0.0f, 0.0f);
+__device__ __forceinline__ float2 sor_ld(const float2 *p) {
+  const uint64_t v = __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(float2, v);
+}
+__device__ __forceinline__ void sor_st(float2 *p, float2 v) {
+  __hip_atomic_store((uint64_t *)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int sor_poll(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave-uniform wait until *p >= need (need is wave-uniform).  Bounded: a
+// producer that never arrives (a bug, never the schedule: producers hold
+// lower tickets) ends the wait after ~2^21 polls with *fail set, so the
+// launch always drains; the host turns *fail into an error.
+__device__ __forceinline__ void sor_wait(const int *p, int need, int &known, int *fail) {
+  for (int n = 0; known < need; ++n) {
+    known = __builtin_amdgcn_readfirstlane(sor_poll(p));
+    if (known >= need) break;
+    if (n > (1 << 21)) {
+      if (threadIdx.x == 0) __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      known = need;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
+}
+// lane l <- lane l-1 / lane l+1 across the whole wave (ds_bpermute-free:
+// row_shr/row_shl cross 16-lane rows only with wave_shr/wave_shl)
+__device__ __forceinline__ float sor_from_up(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float sor_from_down(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+
+// one strip of one half: PH 0 relaxes u (x.x), PH 1 relaxes v (x.y)
+template <int PH>
+__device__ __forceinline__ void sor_strip(const SorArgs &a, int s, int k, double &dn, double &xn) {
+  const int lane = threadIdx.x, H = a.H, W = a.W, P = a.P;
+  const int i0 = s * 64, i = i0 + lane;
+  const bool rowok = i < H;
+  const size_t ps = a.ps;
+  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
+  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
+  const size_t row = (size_t)(rowok ? i : 0) * P;
+  const bool has_up = s > 0, has_dn = i0 + 64 < H;
+  const size_t row_up = (size_t)(has_up ? i0 - 1 : 0) * P, row_dn = (size_t)(has_dn ? i0 + 64 : 0) * P;
+  const int nsteps = W + 63;
+  const int base = k * a.stride;
+  int *my = a.prog + PH * SOR_MAXS + s;
+  const int *pup = a.prog + PH * SOR_MAXS + (s > 0 ? s - 1 : 0);
+  const int *pu = a.prog + s;  // v half: the u strip of the same rows
+  int known_up = 0, known_u = 0;
+  const float om = a.omega, om1 = 1.0f - a.omega;
+
+  // prefetch ring: column j of lane l lives in slot (j + l) & 7 = t & 7
+  float2 X[8], XU[8], XD[8];
+  float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
+  auto fetch = [&](int t) {  // column t + SOR_D - lane
+    const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
+    // wave-uniform waits before reading relaxed values of other strips
+    // lane 0 reads row i0-1 at column tp: strip s-1's lane 63 relaxes it at
+    // its step tp + 63
+    if (has_up && tp >= 0 && tp < W) sor_wait(pup, base + tp + 64, known_up, a.fail);
+    // v half: lane l reads the relaxed u of (i0 + l, tp - l), done at the u
+    // strip's step tp
+    if (PH == 1 && tp >= 0 && tp < nsteps) sor_wait(pu, base + tp + 1, known_u, a.fail);
+    const bool ok = rowok && jp >= 0 && jp < W;
+    const size_t o = row + (ok ? jp : 0);
+    X[q] = ok ? sor_ld(a.x + o) : make_float2(0.f, 0.f);
+    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
+    WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
+    DG[q] = ok ? dgp[o] : 0.f;
+    CC[q] = ok ? ccp[o] : 0.f;
+    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
+    if (lane == 0) {
+      const bool u = has_up && jp >= 0 && jp < W;
+      XU[q] = u ? sor_ld(a.x + row_up + jp) : make_float2(0.f, 0.f);
+      WYU[q] = u ? wyp[row_up + jp] : 0.f;
+    }
+    if (lane == 63) {
+      const bool d = has_dn && jp >= 0 && jp < W;
+      XD[q] = d ? sor_ld(a.x + row_dn + jp) : make_float2(0.f, 0.f);
+    }
+  };
+#pragma unroll
+  for (int t = -SOR_D; t < 0; ++t) fetch(t);
+
+  float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
+  for (int t0 = 0; t0 < nsteps; t0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u;
+      if (t >= nsteps) break;
+      fetch(t);
+      const int j = t - lane, q = t & 7, q1 = (t + 1) & 7;
+      const bool act = rowok && j >= 0 && j < W;
+      const float2 xo = X[q];
+      const float old = PH ? xo.y : xo.x, other = PH ? xo.x : xo.y;
+      // right neighbour: this lane's next point (not yet relaxed)
+      const float right = PH ? X[q1].y : X[q1].x;
+      // down neighbour: lane l+1's next point; the last lane reads strip s+1
+      float down = sor_from_down(right);
+      if (lane == 63) down = PH ? XD[q].y : XD[q].x;
+      // up neighbour: lane l-1's point of the previous step; lane 0 strip s-1
+      float up = sor_from_up(res), wu = sor_from_up(wy_prev);
+      if (lane == 0) {
+        up = PH ? XU[q].y : XU[q].x;
+        wu = WYU[q];
+      }
+      const float sgm = BB[q] + wx_prev * res + WX[q] * right + WY[q] * down + wu * up - CC[q] * other;
+      const float dg = DG[q];
+      float nw = fabsf(dg) < 1e-15f ? old : om1 * old + om * sgm / dg;
+      if (act) {
+        const size_t o = row + j;
+        sor_st(a.x + o, PH ? make_float2(other, nw) : make_float2(nw, other));
+        const double dd = (double)nw - (double)old;
+        dn += dd * dd;
+        xn += (double)nw * nw;
+      } else {
+        nw = 0.f;
+      }
+      res = nw;
+      wx_prev = act ? WX[q] : 0.f;
+      wy_prev = act ? WY[q] : 0.f;
+      if (((t + 1) & (SOR_G - 1)) == 0 || t + 1 == nsteps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(my, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_sor_lex(SorArgs a, int k) {
+  __shared__ int s_exit;
+  const int lane = threadIdx.x;
+  const int nb = 2 * a.nstrips;
+  int tk = 0;
+  if (lane == 0) tk = (int)atomicAdd(a.ticket, 1u) - k * nb;
+  tk = __builtin_amdgcn_readfirstlane(__shfl(tk, 0, 64));
+  if (lane == 0) {
+    int done = a.st->done ? -1 : 0;
+    if (!done && k > 0) {
+      double dn = 0.0, xn = 0.0;
+      for (int b = 0; b < nb; ++b) {  // fixed order: identical in every block
+        dn += a.part_rd[2 * b];
+        xn += a.part_rd[2 * b + 1];
+      }
+      done = sqrt(dn) < a.tol * sqrt(xn) ? 1 : (k >= a.maxiter ? 2 : 0);
+      if (tk == 0) {
+        a.st->iter = k;
+        a.st->rr = dn;
+        a.st->xnorm2 = xn;
+        if (done) a.st->done = done;
+      }
+    }
+    s_exit = done;
+  }
+  __syncthreads();
+  if (s_exit) return;
+  double dn = 0.0, xn = 0.0;
+  const int ph = tk >= a.nstrips ? 1 : 0, s = ph ? tk - a.nstrips : tk;
+  if (ph) sor_strip<1>(a, s, k, dn, xn);
+  else sor_strip<0>(a, s, k, dn, xn);
+  dn = wave_sum(dn);
+  xn = wave_sum(xn);
+  if (lane == 0) {
+    const int slot = ph * a.nstrips + s;  // fixed slot per strip: deterministic sums
+    a.part_wr[2 * slot] = dn;
+    a.part_wr[2 * slot + 1] = xn;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_sor_init(SorArgs a) {
+  for (int e = threadIdx.x + blockIdx.x * 64; e < a.H * a.P; e += gridDim.x * 64) a.x[e] = make_float2(0.f, 0.f);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.st->iter = 0;
     a.st->maxiter = a.maxiter;
     a.st->done = a.maxiter <= 0 ? 2 : 0;
   }
 }
 
-__global__ __launch_bounds__(256) void k_sor_sweep(SorArgs a, int color, int k) {
-  __shared__ double lds[32];
-  __shared__ int s_exit;
-  if (a.st->done) return;
-  if (color == 0 && k > 0) {
-    double s[4];
-    prologue_sum<4>(s, a.part, a.nb, lds);  // red dn, red xn, black dn, black xn of sweep k-1
-    if (threadIdx.x == 0 && threadIdx.y == 0) {
-      const double dn = s[0] + s[2], xn = s[1] + s[3];
-      int done = sqrt(dn) < (double)a.tol * sqrt(xn) ? 1 : (k >= a.maxiter ? 2 : 0);
-      if (blockIdx.x == 0 && blockIdx.y == 0) {
-        a.st->iter = k;
-        a.st->rr = dn;
-        if (done) a.st->done = done;
-      }
-      s_exit = done;
-    }
-    __syncthreads();
-    if (s_exit) return;
+// after the last enqueued sweep k-1: its stopping test (1 wave)
+__global__ __launch_bounds__(64) void k_sor_final(SorArgs a, int k) {
+  if (threadIdx.x != 0 || a.st->done) return;
+  double dn = 0.0, xn = 0.0;
+  for (int b = 0; b < 2 * a.nstrips; ++b) {
+    dn += a.part_rd[2 * b];
+    xn += a.part_rd[2 * b + 1];
   }
-  double v[2] = {0.0, 0.0};
-  const float *wxu = a.coef, *wyu = a.coef + a.ps, *wxv = a.coef + 2 * a.ps, *wyv = a.coef + 3 * a.ps;
-  OF_FOR_PIXELS(a.H, a.W) {
-    if (j >= a.W || ((i + j) & 1) != color) continue;
-    const int W = a.W, H = a.H, P = a.P;
-    const size_t kk = (size_t)i * P + j;
-    float2 s = a.b[kk];
-    if (j < W - 1) { const float2 n = a.x[kk + 1]; s.x += wxu[kk] * n.x; s.y += wxv[kk] * n.y; }
-    if (j > 0) { const float2 n = a.x[kk - 1]; s.x += wxu[kk - 1] * n.x; s.y += wxv[kk - 1] * n.y; }
-    if (i < H - 1) { const float2 n = a.x[kk + P]; s.x += wyu[kk] * n.x; s.y += wyv[kk] * n.y; }
-    if (i > 0) { const float2 n = a.x[kk - P]; s.x += wyu[kk - P] * n.x; s.y += wyv[kk - P] * n.y; }
-    const float aa = a.coef[4 * a.ps + kk], c = a.coef[5 * a.ps + kk], d = a.coef[6 * a.ps + kk];
-    const float det = aa * d - c * c;
-    float2 y;
-    if (det > 1e-30f * fabsf(aa * d)) y = make_float2((d * s.x - c * s.y) / det, (aa * s.y - c * s.x) / det);
-    else y = make_float2(fabsf(aa) > 1e-15f ? s.x / aa : 0.0f, fabsf(d) > 1e-15f ? s.y / d : 0.0f);
-    const float2 o = a.x[kk];
-    const float2 nw = make_float2(o.x + a.omega * (y.x - o.x), o.y + a.omega * (y.y - o.y));
-    a.x[kk] = nw;
-    v[0] += (double)(nw.x - o.x) * (nw.x - o.x) + (double)(nw.y - o.y) * (nw.y - o.y);
-    v[1] += (double)nw.x * nw.x + (double)nw.y * nw.y;
-  }
-  write_partials<2>(v, a.part + (size_t)color * 2 * PCG_MAX_BLOCKS, lds);
-}
-
-__global__ __launch_bounds__(256) void k_sor_final(SorArgs a, int k) {
-  __shared__ double lds[32];
-  if (a.st->done) return;
-  double s[4];
-  prologue_sum<4>(s, a.part, a.nb, lds);
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
-    const double dn = s[0] + s[2], xn = s[1] + s[3];
-    a.st->iter = k;
-    a.st->rr = dn;
-    a.st->done = sqrt(dn) < (double)a.tol * sqrt(xn) ? 1 : 2;
-  }
+  a.st->iter = k;
+  a.st->rr = dn;
+  a.st->xnorm2 = xn;
+  a.st->done = sqrt(dn) < a.tol * sqrt(xn) ? 1 : 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -1561,4 +1282,56 @@ __global__ __launch_bounds__(256) void k_norm2_final(const double *part, int nb,
   double s[1];
   prologue_sum<1>(s, part, nb, lds);
   if (threadIdx.x == 0 && threadIdx.y == 0) *result = s[0];
+}
+
+// ---------------------------------------------------------------------------
+// Diagnostic: the TRUE residual of a solve, ||b - A x||^2 and ||b||^2 in
+// fp64 (A = D - N from the fp32 coefficient planes), independent of any
+// solver recurrence.  Per-block partials, then a one-block finish into
+// out[0..1].
+__global__ __launch_bounds__(256) void k_resid_part(const float *__restrict__ coef, size_t ps,
+                                                    const float2 *__restrict__ b, const float2 *__restrict__ x,
+                                                    int H, int W, int P, double *part) {
+  __shared__ double lds[64];
+  double v[2] = {0.0, 0.0};
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const float2 xc = x[k], bb = b[k];
+    double su = (double)coef[4 * ps + k] * xc.x + (double)coef[5 * ps + k] * xc.y;
+    double sv = (double)coef[5 * ps + k] * xc.x + (double)coef[6 * ps + k] * xc.y;
+    if (j + 1 < W) {
+      const float2 n = x[k + 1];
+      su -= (double)coef[k] * n.x;
+      sv -= (double)coef[2 * ps + k] * n.y;
+    }
+    if (j > 0) {
+      const float2 n = x[k - 1];
+      su -= (double)coef[k - 1] * n.x;
+      sv -= (double)coef[2 * ps + k - 1] * n.y;
+    }
+    if (i + 1 < H) {
+      const float2 n = x[k + P];
+      su -= (double)coef[ps + k] * n.x;
+      sv -= (double)coef[3 * ps + k] * n.y;
+    }
+    if (i > 0) {
+      const float2 n = x[k - P];
+      su -= (double)coef[ps + k - P] * n.x;
+      sv -= (double)coef[3 * ps + k - P] * n.y;
+    }
+    const double ru = (double)bb.x - su, rv = (double)bb.y - sv;
+    v[0] += ru * ru + rv * rv;
+    v[1] += (double)bb.x * bb.x + (double)bb.y * bb.y;
+  }
+  write_partials<2>(v, part, lds);
+}
+__global__ __launch_bounds__(256) void k_resid_final(const double *part, int nb, double *out) {
+  __shared__ double lds[64];
+  double s[2];
+  prologue_sum<2>(s, part, nb, lds);
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    out[0] = s[0];
+    out[1] = s[1];
+  }
 }

@@ -74,6 +74,20 @@ class OfStats(C.Structure):
         }
 
 
+class OfCgGeometry(C.Structure):
+    _fields_ = [("grid_x", C.c_int32), ("grid_y", C.c_int32), ("rows", C.c_int32), ("bands", C.c_int32),
+                ("blocks", C.c_int32), ("strip_cols", C.c_int32)]
+
+
+class OfSolveRecord(C.Structure):
+    _fields_ = [("h", C.c_int32), ("w", C.c_int32), ("solver", C.c_int32), ("iters", C.c_int32),
+                ("done", C.c_int32), ("pad_", C.c_int32), ("true_rel", C.c_double), ("est_rel", C.c_double)]
+
+    def as_dict(self):
+        return {"h": self.h, "w": self.w, "solver": self.solver, "iters": self.iters, "done": self.done,
+                "true_rel": self.true_rel, "est_rel": self.est_rel}
+
+
 def penalty(kind, p0=1.0, p1=0.0):
     return OfPenalty(PENALTY[kind], 0, float(p0), float(p1))
 

@@ -10,7 +10,8 @@ import threading
 
 import numpy as np
 
-from optical_flow._abi import OfParams, OfStats, OF_ABI_VERSION, OF_EINVAL, OF_ENOTSUP
+from optical_flow._abi import (OfParams, OfStats, OfCgGeometry, OfSolveRecord, OF_ABI_VERSION, OF_EINVAL,
+                               OF_ENOTSUP)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OPTFLOW_LIB", os.path.join(_HERE, "_lib", "liboptflow.so"))
@@ -59,6 +60,9 @@ _SIGS = {
     "of_detect_occlusion": ([_vp, _fp, _fp, C.c_int, C.c_int, C.c_int, _fp], C.c_int),
     "of_weighted_median": ([_vp, _fp, _fp, C.c_int, _fp, C.c_int, C.c_int, C.c_int, C.c_double, _fp], C.c_int),
     "of_median_filter": ([_vp, _fp, C.c_int, C.c_int, C.c_int, C.c_int, _fp], C.c_int),
+    "of_solver_geometry": ([C.c_int, C.c_int, C.c_int, C.POINTER(OfCgGeometry)], C.c_int),
+    "of_set_solve_log": ([_vp, C.c_int], C.c_int),
+    "of_solve_log": ([_vp, C.c_int, C.POINTER(OfSolveRecord), _ip], C.c_int),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -116,6 +120,18 @@ class Context:
             raise NotImplementedError(msg)
         raise NativeError(msg)
 
+    def set_solve_log(self, enable=True):
+        """Log the fp64 true residual of every linear solve (of_set_solve_log)."""
+        self.check(self.lib.of_set_solve_log(self.handle, int(bool(enable))))
+
+    def solve_log(self):
+        """Records of the solves since set_solve_log(True) (of_solve_log)."""
+        n = C.c_int(0)
+        self.check(self.lib.of_solve_log(self.handle, 0, None, C.byref(n)))
+        recs = (OfSolveRecord * max(1, n.value))()
+        self.check(self.lib.of_solve_log(self.handle, n.value, recs, C.byref(n)))
+        return [recs[i].as_dict() for i in range(n.value)]
+
     def close(self):
         if self.handle:
             self.lib.of_ctx_destroy(self.handle)
@@ -126,6 +142,20 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def solver_geometry(H, W, solver):
+    """Launch geometry of the solver kernels for an H x W level (of_solver_geometry;
+    no device needed).  Raises NotImplementedError when the level is too large."""
+    from optical_flow._abi import SOLVER
+    lib = load_library()
+    g = OfCgGeometry()
+    rc = lib.of_solver_geometry(int(H), int(W), SOLVER[solver], C.byref(g))
+    if rc == OF_EINVAL:
+        raise ValueError(f"bad geometry request {H}x{W} {solver}")
+    if rc == OF_ENOTSUP:
+        raise NotImplementedError(f"{H}x{W} is too large for the {solver} kernels")
+    return {f: getattr(g, f) for f, _ in OfCgGeometry._fields_}
 
 
 def context():

@@ -296,6 +296,8 @@ class BaseOpticalFlow(ABC):
         ctx = nat.context()
         ctx.check(ctx.lib.of_solve(ctx.handle, C.byref(P), nat.ptr(nat.f32(coef)), nat.ptr(nat.f32(rhs)), H, W,
                                    nat.ptr(x), C.byref(it), C.byref(rr)))
+        # iterations (CG) / sweeps (SOR) and the solver's own residual estimate
+        self.last_solve = {"iters": it.value, "rel_residual": rr.value}
         return nat.interleaved(x).reshape(uv_shape)
 
 

@@ -21,7 +21,6 @@ import numpy as np
 REF = os.environ.get("OF_REFERENCE", "/root/reference")
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REF)
-sys.path.insert(0, os.path.join(HERE, "..", "..", "optical-flow-python_amd"))
 
 from PIL import Image  # noqa: E402
 
@@ -265,6 +264,74 @@ def gen_rubberwhale():
         out[m + ":seconds"] = np.array(time.time() - t0)
         print(f"  {m}: {time.time()-t0:.1f}s")
     save("rubberwhale_ref.npz", **out)
+
+
+def gen_sor():
+    """The reference's lexicographic SOR (base.py:138-172: omega 1.9, tol 1e-2,
+    x0 = 0) on operators of operator.npz, with its sweep count (counted as
+    the norm pairs of its stopping test)."""
+    from optical_flow.methods.base import BaseOpticalFlow
+    from scipy import sparse
+    d = np.load(os.path.join(HERE, "operator.npz"))
+    H, W = d["uv"].shape[:2]
+    n = 2 * H * W
+    out = {}
+    for tag in ("hs", "ba_lor", "nl_robust"):
+        A = sparse.coo_matrix((d[tag + "_val"], (d[tag + "_row"], d[tag + "_col"])), shape=(n, n)).tocsr()
+        calls = [0]
+        norm = np.linalg.norm
+
+        def counting_norm(*a, **k):
+            calls[0] += 1
+            return norm(*a, **k)
+        np.linalg.norm = counting_norm
+        try:
+            x = BaseOpticalFlow._sor_solve(None, A, d[tag + "_b"], 1.9, 10000, 1e-2)
+        finally:
+            np.linalg.norm = norm
+        out[tag + "_x"] = x
+        out[tag + "_sweeps"] = np.array(calls[0] // 2)
+        print(f"  sor {tag}: {calls[0] // 2} sweeps")
+    save("sor.npz", **out)
+
+
+def _aepe(uv, gt):
+    return float(np.mean(np.sqrt(((uv - gt) ** 2).sum(-1))))
+
+
+def _full(name, H, W, method, params, sub):
+    """Reference run on synth_pair(H, W, 0) (BASELINE.json configs 2-4).
+    uv is stored fp32, subsampled by `sub` in both axes (uv[::sub, ::sub]);
+    AEPE against the analytic GT is computed on the full field."""
+    im1, im2, gt = synthetic.synth_pair(H, W, 0)
+    t0 = time.time()
+    uv = quiet(ref.estimate_flow, im1, im2, method, params)
+    sec = time.time() - t0
+    print(f"  {method} {params} {H}x{W}: {sec:.1f}s  AEPE {_aepe(uv, gt):.6f}")
+    save(name, **{f"uv_sub{sub}": uv[::sub, ::sub].astype(np.float32), "seconds": np.array(sec),
+                  "aepe_gt": np.array(_aepe(uv, gt)), "method": np.array(method),
+                  "solver": np.array((params or {}).get("solver", "backslash"))})
+
+
+def gen_full720():
+    """config 3: Classic-C on 1280x720, PCG (ba.py:57-138, base.py:116-136); ~8 min here."""
+    _full("ref720_classic_c_pcg_sub4.npz", 720, 1280, "classic-c", {"solver": "pcg"}, 4)
+
+
+def gen_full1080pcg():
+    """config 4 with solver='pcg' (classic_nl.py:89-198); ~14 min here."""
+    _full("ref1080_pcg_sub4.npz", 1080, 1920, "classic+nl-fast", {"solver": "pcg"}, 4)
+
+
+def gen_full1080():
+    """config 4 with the reference default solver (spsolve, base.py:107-108); ~1-2 h here."""
+    _full("ref1080_backslash_sub4.npz", 1080, 1920, "classic+nl-fast", None, 4)
+
+
+def gen_full480sor():
+    """config 2: 'hs' on 640x480 with the reference's lexicographic SOR (base.py:138-172,
+    a pure-Python row loop); ~1-2 h here."""
+    _full("ref480_hs_sor_sub2.npz", 480, 640, "hs", {"solver": "sor"}, 2)
 
 
 if __name__ == "__main__":

@@ -193,3 +193,26 @@ def test_synthetic_pair_deterministic():
     assert np.array_equal(a1, b1) and np.array_equal(a2, b2)
     assert a1.shape == (24, 40, 3) and g.shape == (24, 40, 2)
     assert a1.min() >= 0 and a1.max() <= 255 and np.all(a1 == np.round(a1))
+
+
+def test_solver_geometry_bounds():
+    """of_solver_geometry (no device): every CG grid fits the partial-sum
+    slots, the loop that sizes k_cg's bands terminates for very wide levels,
+    and levels wider than the slots allow are refused, not mis-sized."""
+    from optical_flow import _native
+    for H, W in [(1080, 1920), (540, 960), (17, 30), (4096, 100), (64, 30000), (1, 1), (7, 57344)]:
+        for solver in ("backslash", "pcg"):
+            g = _native.solver_geometry(H, W, solver)
+            assert 1 <= g["blocks"] == g["grid_x"] * g["grid_y"] <= 512, (H, W, solver, g)
+            assert g["grid_x"] * g["strip_cols"] >= W
+            per_block = 1 if solver == "backslash" else 4
+            assert g["bands"] * g["rows"] >= H and g["grid_y"] * per_block >= g["bands"]
+    for solver in ("backslash", "pcg"):
+        with pytest.raises(NotImplementedError):
+            _native.solver_geometry(64, 124 * 513, solver)
+    g = _native.solver_geometry(480, 640, "sor")
+    assert g["blocks"] == 2 * 8 and g["rows"] == 64
+    with pytest.raises(NotImplementedError):
+        _native.solver_geometry(64 * 257, 100, "sor")
+    with pytest.raises(ValueError):
+        _native.solver_geometry(0, 10, "pcg")

@@ -144,18 +144,46 @@ def test_solve_backslash_and_pcg(golden, tag, meth, alpha):
     assert np.linalg.norm(xf - xs) <= 2e-2 * np.linalg.norm(xs)
 
 
-def test_sor_converges_to_direct(golden):
+@pytest.mark.parametrize("tag,meth", [("hs", "hs"), ("ba_lor", "ba"), ("nl_robust", "classic+nl")])
+def test_sor_matches_reference_sor(golden, tag, meth):
+    """'sor' is the reference's own lexicographic SOR (base.py:138-172), not a
+    reordering: same sweep count and the same iterate as the reference's
+    Python row loop (tests/golden/sor.npz) to fp32 rounding."""
     from optical_flow.methods.config import load_of_method
-    d = golden("operator.npz")
+    d, s = golden("operator.npz"), golden("sor.npz")
     H, W = d["uv"].shape[:2]
+    o = load_of_method(meth)
+    o.solver = "sor"
+    Ar = _ref_A(d, tag, 2 * H * W)
+    x = o._solve_linear_system(Ar, d[tag + "_b"], (H, W, 2))
+    xf = np.concatenate([x[..., 0].ravel(order="F"), x[..., 1].ravel(order="F")])
+    xr = s[tag + "_x"]
+    assert o.last_solve["iters"] == int(s[tag + "_sweeps"]), (o.last_solve, int(s[tag + "_sweeps"]))
+    err = np.linalg.norm(xf - xr) / np.linalg.norm(xr)
+    assert err <= 2e-5, err
+
+
+@pytest.mark.parametrize("H,W", [(40, 56), (64, 64), (150, 200), (200, 131), (300, 90)])
+def test_sor_synthetic_vs_oracle(H, W):
+    """Multi-strip SOR launches (64-row strips handing rows to each other
+    inside one launch) vs the float64 oracle's lexicographic SOR on random
+    flow systems: same sweep count (+-1 at the stopping threshold), same x to
+    fp32 rounding."""
+    import oracle as Or
+    from optical_flow.methods.config import load_of_method
+    from optical_flow.methods.base import sparse_to_planes
+    A, b = _spd_flow_system(H, W, seed=7 * H + W)
     o = load_of_method("hs")
     o.solver = "sor"
-    Ar = _ref_A(d, "hs", 2 * H * W)
-    x = o._solve_linear_system(Ar, d["hs_b"], (H, W, 2))
-    xf = np.concatenate([x[..., 0].ravel(order="F"), x[..., 1].ravel(order="F")])
-    xr = d["hs_x"]
-    # the reference's own SOR stops at ||dx|| < 1e-2 ||x||: a loose solve
-    assert np.linalg.norm(xf - xr) <= 5e-2 * np.linalg.norm(xr)
+    x = o._solve_linear_system(A, b, (H, W, 2))
+    coef = sparse_to_planes(A, H, W)
+    rhs = np.stack([b[:H * W].reshape(H, W, order="F"), b[H * W:].reshape(H, W, order="F")])
+    P = o.to_params()
+    xo, it, _ = Or.solve(P, coef, rhs)
+    assert abs(o.last_solve["iters"] - it) <= 1, (o.last_solve, it)
+    xg = np.moveaxis(x, 2, 0)
+    err = np.linalg.norm(xg - xo) / np.linalg.norm(xo)
+    assert err <= 1e-4, err
 
 
 def test_occlusion(golden):

@@ -201,3 +201,25 @@ def test_e2e_synth_hs(golden):
     d = golden("e2e_synth.npz")
     s = epe_stats(O.estimate_flow(d["im1"], d["im2"], "hs-brightness"), d["hs-brightness"])
     assert s["max"] < 1e-6, s
+
+
+@pytest.mark.parametrize("tag", ["hs", "ba_lor", "nl_robust"])
+def test_oracle_sor_matches_reference(golden, tag):
+    """The oracle's lexicographic SOR (base.py:138-172) reproduces the
+    reference's Python row loop: same sweep count, x to 1e-10."""
+    from scipy import sparse
+    from optical_flow.methods.base import sparse_to_planes
+    from optical_flow.methods.config import load_of_method
+    d, s = golden("operator.npz"), golden("sor.npz")
+    H, W = d["uv"].shape[:2]
+    n = 2 * H * W
+    A = sparse.coo_matrix((d[tag + "_val"], (d[tag + "_row"], d[tag + "_col"])), shape=(n, n)).tocsr()
+    coef = sparse_to_planes(A, H, W)
+    b = d[tag + "_b"]
+    rhs = np.stack([b[:H * W].reshape(H, W, order="F"), b[H * W:].reshape(H, W, order="F")])
+    o = load_of_method("hs")
+    o.solver = "sor"
+    x, it, _ = O.solve(o.to_params(), coef, rhs)
+    xf = np.concatenate([x[0].ravel(order="F"), x[1].ravel(order="F")])
+    assert it == int(s[tag + "_sweeps"])
+    assert np.linalg.norm(xf - s[tag + "_x"]) <= 1e-10 * np.linalg.norm(s[tag + "_x"])
