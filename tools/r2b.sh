@@ -1,0 +1,6 @@
+set -u
+export PYTHONDONTWRITEBYTECODE=1
+mkdir -p gpurun_out
+tools/gpu_step.sh 900 gpurun_out/r2b_gpu.log python -u -m pytest -v -rA --timeout 300 --timeout-method thread tests -m gpu && \
+tools/gpu_step.sh 200 gpurun_out/r2b_smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" && \
+tools/gpu_step.sh 400 gpurun_out/r2b_bench.log python -u bench.py
