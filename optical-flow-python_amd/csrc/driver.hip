@@ -885,21 +885,23 @@ void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &
   REQUIRE(guide.C == 1 || guide.C == 3, OF_ENOTSUP, "weighted median guide must have 1 or 3 channels");
   REQUIRE(hsz >= 0 && hsz <= 12, OF_ENOTSUP, "area_hsz must be <= 12");
   const int RW = WMF_T + 2 * hsz, nreg = RW * RW;
+  const int RP = RW + ((8 - RW) % 16 + 16) % 16;  // record row pitch, RP % 16 == 8 (conflict-free window reads)
   int npow2 = 64;
   while (npow2 < nreg) npow2 <<= 1;
   const int nper = npow2 / 64;  // sort keys per lane: 1..16
-  const size_t shm = 2 * (size_t)npow2 * sizeof(uint16_t) + (size_t)nreg * (guide.C == 3 ? 16 : 8);
+  const size_t shm = 2 * WMF_NC * 64 * sizeof(double) + (size_t)RW * RP * (guide.C == 3 ? 16 : 8) +
+                     2 * (size_t)npow2 * sizeof(uint16_t) + 2 * (size_t)RW * RP;
   dim3 grid((uv.W + WMF_T - 1) / WMF_T, (uv.H + WMF_T - 1) / WMF_T);
   const float nk = (float)(-1.4426950408889634 / (2.0 * sigma_i * sigma_i));  // -log2(e) / (2 sigma^2)
-  auto pick = [&](auto k1, auto k2, auto k4, auto k8, auto k16) {
-    auto k = nper == 1 ? k1 : nper == 2 ? k2 : nper == 4 ? k4 : nper == 8 ? k8 : k16;
+  auto pick = [&](auto k1, auto k2, auto k4, auto k8, auto k8h7, auto k16) {
+    auto k = nper == 1 ? k1 : nper == 2 ? k2 : nper == 4 ? k4 : nper == 8 ? (hsz == 7 ? k8h7 : k8) : k16;
     launch(c, "wmf", k, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H, uv.W,
-           uv.P, guide.ps(), hsz, nk, RW, nreg);
+           uv.P, guide.ps(), hsz, nk, RW, RP);
   };
   if (guide.C == 3)
-    pick(k_wmf<3, 1>, k_wmf<3, 2>, k_wmf<3, 4>, k_wmf<3, 8>, k_wmf<3, 16>);
+    pick(k_wmf<3, 1, 0>, k_wmf<3, 2, 0>, k_wmf<3, 4, 0>, k_wmf<3, 8, 0>, k_wmf<3, 8, 7>, k_wmf<3, 16, 0>);
   else
-    pick(k_wmf<1, 1>, k_wmf<1, 2>, k_wmf<1, 4>, k_wmf<1, 8>, k_wmf<1, 16>);
+    pick(k_wmf<1, 1, 0>, k_wmf<1, 2, 0>, k_wmf<1, 4, 0>, k_wmf<1, 8, 0>, k_wmf<1, 8, 7>, k_wmf<1, 16, 0>);
 }
 
 void resample_f2(of_ctx *c, const F2 &in, const F2 &out) {

@@ -369,55 +369,89 @@ __global__ void k_lo_blend(const float2 *__restrict__ u, const float2 *__restric
 // (denoise_color_weighted_medfilt2, weighted_median.py:24-112).  One wave per 8x8 tile:
 //  1. the (8+2h)^2 region is loaded straight into registers, NPER keys per
 //     lane (element e = lane*NPER + r), and guide+occ records go to LDS;
-//  2. u and v keys are bitonic-sorted in registers: stages with partner
-//     distance < NPER swap registers, the others exchange with lane^(d/NPER)
-//     by ds_bpermute (no LDS storage, no barriers);
-//  3. sorted keys go to LDS; every lane walks both lists in lockstep, 8 keys
-//     per batch, weights of the u and v samples computed in packed fp32
-//     (v_pk_*), fp64 cumulative sums advanced branch-free in sorted order.
+//  2. u and v keys (order-preserving value bits << 32 | region position) are
+//     bitonic-sorted in registers; each sample's sorted index e gives it a
+//     chunk id e / CH (WMF_NC chunks of CH consecutive sorted samples per list);
+//  3. every lane visits its own 15x15 window once (no out-of-window work):
+//     weight w is added to the lane's chunk sums of the u and v lists
+//     (ds_add_f64 into lane-private LDS slots, program order ->
+//     deterministic); the window total is the sum of the chunk sums;
+//  4. the chunk holding the half-weight crossing is found from the chunk
+//     prefix sums; only that chunk's CH sorted samples are walked (per-lane
+//     addresses) to the first one whose cumulative weight reaches total/2.
+// LDS per wave at h = 7: 8 KB chunk sums + 8.4 KB records + 2 KB sorted
+// positions + 1 KB chunk ids = 19.3 KB -> 8 waves per CU.
 // Weight = max(2^(-|dlab|^2 * log2e/(2 sigma^2)) * occ, 1e-10) (v_exp_f32);
 // result = the first sorted value with cumsum >= total/2
-// (weighted_median.py:5-21, :67-112).
+// (weighted_median.py:5-21, :67-112): the cumulative sum at a sorted sample
+// is (chunk prefix) + (in-window weights before it in the chunk), the same
+// sums the reference forms, summed in another order.
 #define WMF_T 8
+#ifdef WMF_PHASE_TIMING  // tools/micro/wmf_phases.hip: per-wave phase timestamps
+extern __device__ unsigned long long g_wmf_t[];
+#define WMF_STAMP(i) \
+  if (threadIdx.x == 0) g_wmf_t[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = clock64()
+#else
+#define WMF_STAMP(i)
+#endif
+#define WMF_NC 8
 template <int GC>
 struct WmfRec;
 template <>
 struct WmfRec<3> {
   using T = float4;
   __device__ static T make(float a, float b, float c, float o) { return make_float4(a, b, c, o); }
-  __device__ static float d2(const T &s, const float *cg) {
-    const float e0 = s.x - cg[0], e1 = s.y - cg[1], e2 = s.z - cg[2];
-    return e0 * e0 + e1 * e1 + e2 * e2;
-  }
-  __device__ static float occ(const T &s) { return s.w; }
 };
 template <>
 struct WmfRec<1> {
   using T = float2;
   __device__ static T make(float a, float, float, float o) { return make_float2(a, o); }
-  __device__ static float d2(const T &s, const float *cg) {
-    const float e0 = s.x - cg[0];
-    return e0 * e0;
-  }
-  __device__ static float occ(const T &s) { return s.y; }
 };
 
 typedef float wmf_v2f __attribute__((ext_vector_type(2)));
 
 // weight of region sample s for a pixel of guide colour (c01, c2):
-// max(2^(nk |dlab|^2) occ, 1e-10), channels 0-1 in packed fp32
+// max(2^(nk |dlab|^2) occ, 1e-10), channels 0-1 in packed fp32.  Called from
+// the window pass and the chunk walk: both must round identically, so no
+// contraction beyond the explicit fma.
 __device__ __forceinline__ float wmf_w(const float4 &s, wmf_v2f c01, float c2, float nk) {
+#pragma clang fp contract(off)
   const wmf_v2f e = wmf_v2f{s.x, s.y} - c01, q = e * e;
   const float e2 = s.z - c2;
-  return fmaxf(__builtin_amdgcn_exp2f(fmaf(e2, e2, q.x + q.y) * nk) * s.w, 1e-10f);
+  return fmaxf(__builtin_amdgcn_exp2f(__builtin_fmaf(e2, e2, q.x + q.y) * nk) * s.w, 1e-10f);
 }
 __device__ __forceinline__ float wmf_w(const float2 &s, wmf_v2f c01, float, float nk) {
+#pragma clang fp contract(off)
   const float e = s.x - c01.x;
   return fmaxf(__builtin_amdgcn_exp2f(e * e * nk) * s.y, 1e-10f);
 }
 
+// v from lane ^ lj: DPP for lj = 1, 2 (quad_perm) and 8 (row_ror:8), a
+// ds_bpermute otherwise (lj is a constant once the sort loops are unrolled)
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lj) {
+  const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+  int a, b;
+  if (lj == 1) {
+    a = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xf, 0xf, false);
+    b = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xf, 0xf, false);
+  } else if (lj == 2) {
+    a = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xf, 0xf, false);
+    b = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xf, 0xf, false);
+  } else if (lj == 8) {
+    a = __builtin_amdgcn_mov_dpp(lo, 0x128, 0xf, 0xf, false);
+    b = __builtin_amdgcn_mov_dpp(hi, 0x128, 0xf, 0xf, false);
+  } else {
+    return __shfl_xor(v, lj);
+  }
+  return ((uint64_t)(uint32_t)b << 32) | (uint32_t)a;
+}
+
+// Bitonic sort of the 64*NPER keys of two lists at once (element e = lane *
+// NPER + r).  Partners at distance >= NPER are in another lane (xor_lane64),
+// the others in the same lane.  The direction of a compare-exchange is a lane
+// mask per stage; one v_cmp_u64 + two v_cndmask per element.
 template <int NPER>
-__device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
+__device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&kb)[NPER], int lane) {
   constexpr int N = NPER * 64;
 #pragma unroll
   for (int kk = 2; kk <= N; kk <<= 1) {
@@ -425,14 +459,13 @@ __device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
     for (int jj = kk >> 1; jj > 0; jj >>= 1) {
       if (jj >= NPER) {
         const int lj = jj / NPER;
-        const bool lower = (lane & lj) == 0;
+        // kk > NPER here: the direction depends on the lane only
+        const bool take_min = ((lane & lj) == 0) == (((lane * NPER) & kk) == 0);
 #pragma unroll
         for (int r = 0; r < NPER; ++r) {
-          const bool up = (((lane * NPER + r) & kk) == 0);
-          const uint64_t o = __shfl_xor(k[r], lj);
-          const bool take_min = lower == up;
-          const uint64_t mn = k[r] < o ? k[r] : o, mx = k[r] < o ? o : k[r];
-          k[r] = take_min ? mn : mx;
+          const uint64_t oa = xor_lane64(ka[r], lj), ob = xor_lane64(kb[r], lj);
+          ka[r] = ((ka[r] < oa) == take_min) ? ka[r] : oa;
+          kb[r] = ((kb[r] < ob) == take_min) ? kb[r] : ob;
         }
       } else {
 #pragma unroll
@@ -440,10 +473,12 @@ __device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
           const int rp = r ^ jj;
           if (rp > r) {
             const bool up = (((lane * NPER + r) & kk) == 0);
-            const uint64_t a = k[r], b = k[rp];
-            const bool sw = (a > b) == up;
-            k[r] = sw ? b : a;
-            k[rp] = sw ? a : b;
+            const uint64_t a0 = ka[r], a1 = ka[rp], b0 = kb[r], b1 = kb[rp];
+            const bool sa = (a0 > a1) == up, sb = (b0 > b1) == up;
+            ka[r] = sa ? a1 : a0;
+            ka[rp] = sa ? a0 : a1;
+            kb[r] = sb ? b1 : b0;
+            kb[rp] = sb ? b0 : b1;
           }
         }
       }
@@ -451,20 +486,31 @@ __device__ __forceinline__ void bitonic_regs(uint64_t (&k)[NPER], int lane) {
   }
 }
 
-template <int GC, int NPER>
-__global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
+// HS > 0: area_hsz fixed at compile time (window loop fully unrolled,
+// immediate LDS offsets); HS == 0: runtime hsz.  RP = LDS row pitch of the
+// region records (RP % 16 == 8: the 8 rows of a tile fall on disjoint banks).
+// LDS (not VGPRs) bounds the occupancy at 2 waves per SIMD: let the
+// scheduler use the registers to keep LDS reads in flight
+template <int GC, int NPER, int HS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
                                              const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
-                                             int P, size_t ps, int hsz, float nk, int RW, int nreg) {
-  using R = WmfRec<GC>;
-  using T = typename R::T;
-  constexpr int N = NPER * 64;
-  // LDS: sorted region positions (ry << 8 | rx) of the u and v lists, then
-  // the guide+occ records: 2*N*2 + nreg*sizeof(T) bytes (9.8 KB at h = 7)
-  extern __shared__ uint64_t lds_u64[];
-  T *smp = reinterpret_cast<T *>(lds_u64);  // [nreg]
-  uint16_t *ku = reinterpret_cast<uint16_t *>(smp + nreg), *kv = ku + N;
+                                             int P, size_t ps, int hsz_rt, float nk, int RW, int RP) {
+  using T = typename WmfRec<GC>::T;
+  constexpr int N = NPER * 64, CH = N / WMF_NC;
+  const int hsz = HS > 0 ? HS : hsz_rt;
+  const int nreg = RW * RW;
+  // LDS: chunk sums [2][WMF_NC][64] f64 (u chunks, then v chunks; a chunk's
+  // 64 lane slots are contiguous, so a scatter-add never conflicts) | records
+  // [RW][RP] | sorted positions (ry << 8 | rx) of the u and v lists [2][N] u16 |
+  // chunk ids [2][RW][RP] u8 (u list, v list)
+  extern __shared__ double lds_f64[];
+  double *csum = lds_f64;
+  T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
+  uint16_t *ku = reinterpret_cast<uint16_t *>(smp + RW * RP), *kv = ku + N;
+  uint8_t *cid = reinterpret_cast<uint8_t *>(kv + N);
   const int ty0 = blockIdx.y * WMF_T, tx0 = blockIdx.x * WMF_T;
   const int lane = threadIdx.x;
+  WMF_STAMP(0);
   uint64_t a[NPER], b[NPER];
 #pragma unroll
   for (int r = 0; r < NPER; ++r) {
@@ -481,82 +527,138 @@ __global__ __launch_bounds__(64) void k_wmf(const float2 *__restrict__ uv, const
       float gv[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < GC; ++c) gv[c] = guide[c * ps + g];
-      smp[s] = R::make(gv[0], gv[1], gv[2], occ[g]);
+      smp[ry * RP + rx] = WmfRec<GC>::make(gv[0], gv[1], gv[2], occ[g]);
     }
   }
-  bitonic_regs<NPER>(a, lane);
-  bitonic_regs<NPER>(b, lane);
+  double *cs = csum + lane;
+#pragma unroll
+  for (int c = 0; c < 2 * WMF_NC; ++c) cs[c * 64] = 0.0;
+  WMF_STAMP(1);
+  bitonic_regs2<NPER>(a, b, lane);
 #pragma unroll
   for (int r = 0; r < NPER; ++r) {
-    ku[lane * NPER + r] = (uint16_t)a[r];  // padding keys -> 0xffff: out of every window
-    kv[lane * NPER + r] = (uint16_t)b[r];
+    const int e = lane * NPER + r;
+    const unsigned pa = (uint16_t)a[r], pb = (uint16_t)b[r];
+    ku[e] = (uint16_t)pa;  // padding keys -> 0xffff: out of every window
+    kv[e] = (uint16_t)pb;
+    if (pa != 0xffffu) cid[(pa >> 8) * RP + (pa & 0xffu)] = (uint8_t)(e / CH);
+    if (pb != 0xffffu) cid[RW * RP + (pb >> 8) * RP + (pb & 0xffu)] = (uint8_t)(e / CH);
   }
   __syncthreads();
+  WMF_STAMP(2);
   const int py = lane >> 3, px = lane & 7;
   const int gi = ty0 + py, gj = tx0 + px;
-  const bool live = gi < H && gj < W;  // dead lanes still walk (wave-uniform exit)
+  const int qb = py * RP + px;
   float cg[3] = {0.f, 0.f, 0.f};
   {
-    const T c0 = smp[(py + hsz) * RW + px + hsz];
+    const T c0 = smp[qb + hsz * RP + hsz];
     const float *cf = reinterpret_cast<const float *>(&c0);
 #pragma unroll
     for (int c = 0; c < GC; ++c) cg[c] = cf[c];
   }
   const wmf_v2f c01 = {cg[0], cg[1]};
-  // total weight of the lane's window (row-major window order)
-  double tot = 0.0;
-  for (int dy = 0; dy <= 2 * hsz; ++dy) {
-    const T *row = smp + (py + dy) * RW + px;
-    for (int dx = 0; dx <= 2 * hsz; ++dx) tot += (double)wmf_w(row[dx], c01, cg[2], nk);
+  // window pass: the per-chunk weight of both lists.  One window row per
+  // step: its records and chunk offsets are read first, so the LDS latency
+  // is paid once per row.
+  char *csb = reinterpret_cast<char *>(cs);
+  auto visit_row = [&](int q0, int n) {
+    constexpr int MX = HS > 0 ? 2 * HS + 1 : 5;
+    T rec[MX];
+    unsigned cu[MX], cv[MX];
+#pragma unroll
+    for (int dx = 0; dx < MX; ++dx)
+      if (dx < n) {
+        rec[dx] = smp[q0 + dx];
+        cu[dx] = cid[q0 + dx];
+        cv[dx] = cid[RW * RP + q0 + dx];
+      }
+#pragma unroll
+    for (int dx = 0; dx < MX; ++dx)
+      if (dx < n) {
+        const double w = (double)wmf_w(rec[dx], c01, cg[2], nk);
+        atomicAdd(reinterpret_cast<double *>(csb + (cu[dx] << 9)), w);
+        atomicAdd(reinterpret_cast<double *>(csb + (cv[dx] << 9)) + WMF_NC * 64, w);
+      }
+  };
+  if (HS > 0) {
+#pragma unroll
+    for (int dy = 0; dy <= 2 * HS; ++dy) visit_row(qb + dy * RP, 2 * HS + 1);
+  } else {
+    for (int dy = 0; dy <= 2 * hsz; ++dy)
+      for (int dx = 0; dx <= 2 * hsz; dx += 5) visit_row(qb + dy * RP + dx, min(5, 2 * hsz + 1 - dx));
+  }
+  WMF_STAMP(3);
+  double su[WMF_NC], sv[WMF_NC], tot = 0.0;
+#pragma unroll
+  for (int c = 0; c < WMF_NC; ++c) {
+    su[c] = cs[c * 64];
+    sv[c] = cs[(WMF_NC + c) * 64];
+    tot += su[c];
   }
   const double half = 0.5 * tot;
-  const unsigned span = 2u * hsz;
-  double cu = 0.0, cv = 0.0;
-  unsigned resu = 0, resv = 0;
-  bool du = !live, dv = !live;
-  for (int k0 = 0; k0 < N; k0 += 8) {
-    // keys are wave-uniform: each sample record is one broadcast LDS read,
-    // the per-lane part is the window test
-    unsigned ka[8], kb[8];
+  // crossing chunk of each list: first chunk whose running sum reaches half
+  double pu = 0.0, pv = 0.0, bu = 0.0, bv = 0.0;
+  int chu = -1, chv = -1, lastu = 0, lastv = 0;
+  double lbu = 0.0, lbv = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      ka[i] = ku[k0 + i];
-      kb[i] = kv[k0 + i];
-    }
-    float wa[8], wb[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu, ryb = kb[i] >> 8, rxb = kb[i] & 0xffu;
-      const bool ina = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
-      const bool inb = (ryb - (unsigned)py) <= span && (rxb - (unsigned)px) <= span;
-      // padding keys (0xffff) are outside every window; read any record
-      const float xa = wmf_w(smp[ka[i] == 0xffffu ? 0u : rya * RW + rxa], c01, cg[2], nk);
-      const float xb = wmf_w(smp[kb[i] == 0xffffu ? 0u : ryb * RW + rxb], c01, cg[2], nk);
-      wa[i] = ina ? xa : 0.0f;
-      wb[i] = inb ? xb : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      cu += (double)wa[i];
-      cv += (double)wb[i];
-      const bool xa = !du && cu >= half, xb = !dv && cv >= half;
-      resu = xa ? ka[i] : resu;
-      resv = xb ? kb[i] : resv;
-      du = du || xa;
-      dv = dv || xb;
-    }
-    if (__all(du && dv)) break;
+  for (int c = 0; c < WMF_NC; ++c) {
+    if (chu < 0 && su[c] > 0.0) { lastu = c; lbu = pu; }
+    if (chv < 0 && sv[c] > 0.0) { lastv = c; lbv = pv; }
+    if (chu < 0 && pu + su[c] >= half) { chu = c; bu = pu; }
+    if (chv < 0 && pv + sv[c] >= half) { chv = c; bv = pv; }
+    pu += su[c];
+    pv += sv[c];
   }
-  if (live) {
+  // rounding of the v chunk sums vs the total: fall back to the last chunk
+  // with window weight (the walk then ends on its last window sample)
+  if (chu < 0) { chu = lastu; bu = lbu; }
+  if (chv < 0) { chv = lastv; bv = lbv; }
+  WMF_STAMP(4);
+  const unsigned span = 2u * hsz;
+  unsigned resu = 0xffffu, resv = 0xffffu, lstu = 0, lstv = 0;
+  // the crossing chunks' sorted positions, 8 per 16-B read
+  const uint4 *wu = reinterpret_cast<const uint4 *>(ku + chu * CH), *wv = reinterpret_cast<const uint4 *>(kv + chv * CH);
+  for (int g = 0; g < CH / 8; ++g) {
+    const uint4 A = wu[g], B = wv[g];
+    const unsigned wa4[4] = {A.x, A.y, A.z, A.w}, wb4[4] = {B.x, B.y, B.z, B.w};
+    unsigned ka[8], kb[8];
+    bool ina[8], inb[8];
+    T ra[8], rb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ka[i] = (wa4[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      kb[i] = (wb4[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu, ryb = kb[i] >> 8, rxb = kb[i] & 0xffu;
+      // padding keys (0xffff) fail the window test (ry = 255)
+      ina[i] = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
+      inb[i] = (ryb - (unsigned)py) <= span && (rxb - (unsigned)px) <= span;
+      ra[i] = smp[ina[i] ? rya * RP + rxa : 0u];
+      rb[i] = smp[inb[i] ? ryb * RP + rxb : 0u];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xa = wmf_w(ra[i], c01, cg[2], nk), xb = wmf_w(rb[i], c01, cg[2], nk);
+      bu += ina[i] ? (double)xa : 0.0;
+      bv += inb[i] ? (double)xb : 0.0;
+      resu = (resu == 0xffffu && ina[i] && bu >= half) ? ka[i] : resu;
+      resv = (resv == 0xffffu && inb[i] && bv >= half) ? kb[i] : resv;
+      lstu = ina[i] ? ka[i] : lstu;
+      lstv = inb[i] ? kb[i] : lstv;
+    }
+  }
+  if (resu == 0xffffu) resu = lstu;
+  if (resv == 0xffffu) resv = lstv;
+  WMF_STAMP(5);
+  if (gi < H && gj < W) {
     // the selected samples' values, re-read at their (mirrored) positions
     const int ya = ext_mirror(ty0 - hsz + (int)(resu >> 8), H), xa = ext_mirror(tx0 - hsz + (int)(resu & 0xffu), W);
     const int yb = ext_mirror(ty0 - hsz + (int)(resv >> 8), H), xb = ext_mirror(tx0 - hsz + (int)(resv & 0xffu), W);
     out[(size_t)gi * P + gj] = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
   }
 }
-#define OF_WMF(GC, NP)                                                                                           \
-  template __global__ void k_wmf<GC, NP>(const float2 *, const float *, const float *, float2 *, int, int, int, \
-                                          size_t, int, float, int, int);
-OF_WMF(1, 1) OF_WMF(1, 2) OF_WMF(1, 4) OF_WMF(1, 8) OF_WMF(1, 16)
-OF_WMF(3, 1) OF_WMF(3, 2) OF_WMF(3, 4) OF_WMF(3, 8) OF_WMF(3, 16)
+#define OF_WMF(GC, NP, HS)                                                                                       \
+  template __global__ void k_wmf<GC, NP, HS>(const float2 *, const float *, const float *, float2 *, int, int, int, \
+                                              size_t, int, float, int, int);
+OF_WMF(1, 1, 0) OF_WMF(1, 2, 0) OF_WMF(1, 4, 0) OF_WMF(1, 8, 0) OF_WMF(1, 16, 0) OF_WMF(1, 8, 7)
+OF_WMF(3, 1, 0) OF_WMF(3, 2, 0) OF_WMF(3, 4, 0) OF_WMF(3, 8, 0) OF_WMF(3, 16, 0) OF_WMF(3, 8, 7)
 #undef OF_WMF

@@ -201,9 +201,35 @@ def test_weighted_median(golden, guide, hsz, sig, key):
     out = denoise_color_weighted_medfilt2(d["uv"], d[guide], d["occ"], hsz, [5, 5], sig)
     ref = d[key]
     same = np.abs(out - ref) <= 1e-6 * (1 + np.abs(ref))
-    # float32 weights / cumulative sums may pick a neighbouring order statistic
-    # when the half-weight crossing is within rounding; everything else exact
-    assert same.mean() >= 0.995, same.mean()
+    # float32 weights may pick a neighbouring order statistic when the
+    # half-weight crossing is within rounding; everything else exact
+    print(f"wmf {key}: exact fraction {same.mean():.5f}")
+    assert same.mean() >= 0.999, same.mean()
+
+
+@pytest.mark.parametrize("gc,hsz,sig", [(3, 7, 7.0), (1, 7, 7.0), (3, 3, 4.0), (3, 12, 7.0)])
+def test_weighted_median_synthetic_vs_oracle(gc, hsz, sig):
+    """Weighted median of a 96x136 synthetic flow (smooth field + noise +
+    a motion edge, so sorted chunks and window crossings vary) against the
+    float64 oracle on the same fp32-rounded inputs: >= 99.9 % of pixels
+    exact, the rest a neighbouring order statistic."""
+    import oracle as Or
+    from optical_flow.utils.weighted_median import denoise_color_weighted_medfilt2
+    from optical_flow.utils.synthetic import synth_pair
+    H, W = 96, 136
+    im1, _, gt = synth_pair(H, W, 5)
+    rng = np.random.default_rng(11)
+    uv = gt + 0.3 * rng.standard_normal(gt.shape)
+    uv[:, W // 2:] += 1.5
+    uv = uv.astype(np.float32).astype(np.float64)
+    guide = (Or.rgb2lab(im1) if gc == 3 else im1.mean(-1)).astype(np.float32).astype(np.float64)
+    occ = rng.uniform(0.0, 1.0, (H, W)).astype(np.float32).astype(np.float64)
+    occ[:20, :30] = 0.0  # weights at the 1e-10 floor
+    out = denoise_color_weighted_medfilt2(uv, guide, occ, hsz, [5, 5], sig)
+    ref = Or.weighted_median(uv, guide, occ, hsz, sig)
+    same = np.abs(out - ref) <= 1e-6 * (1 + np.abs(ref))
+    print(f"wmf synthetic gc={gc} hsz={hsz}: exact fraction {same.mean():.5f}")
+    assert same.mean() >= 0.999, same.mean()
 
 
 def test_weighted_median_no_guide_is_median(golden):

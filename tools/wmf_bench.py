@@ -26,8 +26,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--gc", type=int, default=3)
     ap.add_argument("--save", default=None)
+    ap.add_argument("--lib", default=None, help="alternative liboptflow.so (variant builds)")
     a = ap.parse_args()
     H, W = a.h, a.w
+    if a.lib:
+        _native._lib = _native.load_library(a.lib)
     im1, _, gt = synth_pair(H, W, 0)
     rng = np.random.default_rng(0)
     uv = (gt + 0.05 * rng.standard_normal(gt.shape)).astype(np.float32)
@@ -48,7 +51,7 @@ def main():
     cnt = (C.c_int64 * 64)()
     ctx.check(lib.of_kernel_times(ctx.handle, 64, names, ms, cnt, None, C.byref(n)))
     rec = {names[i].decode(): ms[i] / cnt[i] for i in range(n.value)}
-    print(json.dumps({"variant": os.environ.get("OF_WMF_VARIANT", "default"), "H": H, "W": W, "gc": a.gc,
+    print(json.dumps({"variant": a.lib or "default", "H": H, "W": W, "gc": a.gc,
                       "ms_per_launch": rec, "sha1": hashlib.sha1(out.tobytes()).hexdigest()}), flush=True)
     if a.save:
         np.save(a.save, out)
