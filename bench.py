@@ -5,13 +5,16 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One process per GPU.  A step = every rank runs estimate_flow on its P
-device-resident pairs (default 8 = config 5's 64 pairs over 8 GPUs; inputs
-uploaded to HBM before timing: RGB -> gray/Lab, ROF, pyramids, GNC x levels
-x IRLS, all on the GPU), L of them in flight on concurrent streams
-(of_pairs_run), and, for N > 1, the flows are gathered to rank 0 with RCCL
-over xGMI.  Timed region: barrier + device sync on both sides, max over
-ranks.  value = pairs processed by all ranks / time (weak scaling: P pairs
-per GPU).
+pairs (default 8 = config 5's 64 pairs over 8 GPUs) HOST TO HOST, as SURVEY.md
+§8d defines the headline: uint8 RGB frames in host memory -> H2D -> RGB ->
+gray/Lab, ROF, pyramids, GNC x levels x IRLS on the GPU -> D2H of the fp32
+flow into host memory (of_pairs_run_host: L pairs in flight on concurrent
+streams, uploads/downloads overlapped with compute on copy streams); for
+N > 1 the flows are also gathered to rank 0 with RCCL over xGMI.  Timed
+region: barrier + device sync on both sides, max over ranks.  value = pairs
+processed by all ranks / time (weak scaling: P pairs per GPU).  The
+device-resident rate (frames already in HBM, flows left there:
+of_pairs_run) is reported beside it as `device_resident`.
 
 Also reported (one JSON line on rank 0):
   roofline      dominant HBM kernel: algorithmic bytes per launch / mean
@@ -66,7 +69,7 @@ def parse():
     ap.add_argument("--solver", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=180, help="crop height of the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=360, help="crop height of the CPU-baseline sample")
     return ap.parse_args()
 
 
@@ -115,6 +118,34 @@ def run_step(ctx, P0, nslots, lanes):
     """estimate_flow on device slots 0..nslots-1, `lanes` pairs in flight
     (each lane its own HIP stream + host thread inside the library)."""
     ctx.check(ctx.lib.of_pairs_run(ctx.handle, nslots, C.byref(P0), lanes, None))
+
+
+def flow_digests(outs):
+    import hashlib
+    return [hashlib.sha1(o.tobytes()).hexdigest() for o in outs]
+
+
+def verify_gather(buf, every, world, pairs):
+    """True iff pair s of rank src sits at offset src * pairs + s of the
+    gathered buffer (of_rccl_gather_flows' layout = shard_seeds' global pair
+    order), by the sha1 digests every rank published for its own flows."""
+    import hashlib
+    return all(hashlib.sha1(buf[src * pairs + s].tobytes()).hexdigest() == every[src][s]
+               for src in range(world) for s in range(pairs))
+
+
+def gather_check(dist, ctx, lib, world, rank, pairs, H, W, outs):
+    """One untimed RCCL gather into a host buffer on rank 0, checked against
+    the digests every rank publishes over gloo; raises on a layout mismatch."""
+    every = [None] * world
+    dist.all_gather_object(every, flow_digests(outs))
+    buf = np.empty((world * pairs, 2, H, W), dtype=np.float32) if rank == 0 else None
+    ctx.check(lib.of_rccl_gather_flows(ctx.handle, pairs, _native.ptr(buf) if rank == 0 else None))
+    flag = [verify_gather(buf, every, world, pairs) if rank == 0 else None]
+    dist.broadcast_object_list(flag, src=0)
+    if not flag[0]:
+        raise RuntimeError("RCCL gather layout check failed")
+    return {"pairs": world * pairs, "layout": "rank r pair s at r*P+s", "ok": True}
 
 
 def cpu_baseline(args):
@@ -197,14 +228,20 @@ def main():
     H, W = args.height, args.width
     P0 = make_params(args)
 
-    # inputs resident in HBM before timing
+    # host frames (uint8, what a caller holds) and host flow buffers; the
+    # same pairs also uploaded once to device slots for the device-resident rate
     seeds = shard_seeds(rank, args.pairs)
-    gts = []
-    for s, seed in enumerate(seeds):
+    gts, f1, f2 = [], [], []
+    for seed in seeds:
         im1, im2, gt = synth_pair(H, W, seed)
         gts.append(gt)
-        a1, a2 = _native.f32(im1), _native.f32(im2)
-        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(a1), _native.ptr(a2), H, W, 3))
+        f1.append(np.ascontiguousarray(im1.astype(np.uint8)))
+        f2.append(np.ascontiguousarray(im2.astype(np.uint8)))
+    outs = [np.empty((2, H, W), dtype=np.float32) for _ in seeds]
+    vp = C.c_void_p
+    p1 = (vp * args.pairs)(*[x.ctypes.data for x in f1])
+    p2 = (vp * args.pairs)(*[x.ctypes.data for x in f2])
+    po = (vp * args.pairs)(*[o.ctypes.data for o in outs])
     if world > 1:
         uid = C.create_string_buffer(128)
         if rank == 0:
@@ -214,7 +251,7 @@ def main():
         ctx.check(lib.of_rccl_init(ctx.handle, obj[0], world, rank))
 
     def step():
-        run_step(ctx, P0, args.pairs, args.lanes)
+        ctx.check(lib.of_pairs_run_host(ctx.handle, args.pairs, p1, p2, H, W, 3, C.byref(P0), args.lanes, po, None))
         if world > 1:
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
 
@@ -229,6 +266,24 @@ def main():
     barrier(dist)
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     value = world * args.pairs * args.steps / elapsed
+    gather = gather_check(dist, ctx, lib, world, rank, args.pairs, H, W, outs) if world > 1 else None
+
+    # device-resident rate: frames uploaded to slots beforehand, flows left in HBM
+    for s, (a, b) in enumerate(zip(f1, f2)):
+        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
+                                     H, W, 3))
+    dsteps = max(1, min(args.steps, 2))
+    barrier(dist)
+    ctx.check(lib.of_synchronize(ctx.handle))
+    t1 = time.perf_counter()
+    for _ in range(dsteps):
+        run_step(ctx, P0, args.pairs, args.lanes)
+    ctx.check(lib.of_synchronize(ctx.handle))
+    barrier(dist)
+    dev_elapsed = max_over_ranks(dist, time.perf_counter() - t1)
+    dev_uv = np.empty((2, H, W), dtype=np.float32)
+    ctx.check(lib.of_pair_download(ctx.handle, 0, _native.ptr(dev_uv)))
+    host_eq_dev = bool(np.array_equal(dev_uv, outs[0]))
 
     # per-level times + accuracy from one more (untimed) pair
     st = _abi.OfStats()
@@ -286,6 +341,11 @@ def main():
                        "lanes": min(args.lanes, args.pairs),
                        "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
                        "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
+            "timed_region": "host to host: uint8 RGB pairs in host memory -> flows (fp32) in host memory",
+            "device_resident": {"value": round(world * args.pairs * dsteps / dev_elapsed, 4),
+                                "ms_per_step": round(1e3 * dev_elapsed / dsteps, 3), "steps": dsteps,
+                                "host_flow_equals_device_flow": host_eq_dev},
+            "gather_check": gather,
             "roofline": roofline, "cpu_baseline": cpu,
             "ms_per_level": [{"stage": l["stage"], "h": l["h"], "w": l["w"], "ms": round(l["ms"], 3)}
                              for l in sd["levels"]],

@@ -189,6 +189,17 @@ int of_pair_run(of_ctx *ctx, int slot, of_params *params, of_stats *stats);
  * slot and not written back; stats (may be NULL) receives slot 0's.  Results
  * are bitwise independent of `lanes`.  Returns when every slot is done. */
 int of_pairs_run(of_ctx *ctx, int nslots, const of_params *params, int lanes, of_stats *stats);
+/* host-to-host batch (the SURVEY.md §8d headline; replaces a Python loop of
+ * estimate_flow(im1[k], im2[k], method) calls, interface.py:11-71): reads
+ * npairs caller-owned (H, W, C) uint8 frame pairs (C = 1 or 3), writes each
+ * pair's flow as planar 2 x H x W fp32 into out_uv[k].  `lanes` pairs in
+ * flight as in of_pairs_run; per lane the H2D of pair j+1's bytes and the
+ * D2H of pair j-1's flow overlap pair j's kernels (pinned double buffers, a
+ * copy stream).  The flows also stay on the device in slots 0..npairs-1
+ * (of_pair_download, of_rccl_gather_flows).  Results equal of_pairs_run on
+ * the same frames (bitwise, independent of `lanes`). */
+int of_pairs_run_host(of_ctx *ctx, int npairs, const uint8_t *const *im1, const uint8_t *const *im2, int H, int W,
+                      int C, const of_params *params, int lanes, float *const *out_uv, of_stats *stats);
 /* D2H of a slot's flow (planar 2 x H x W) */
 int of_pair_download(of_ctx *ctx, int slot, float *out_uv);
 

@@ -98,9 +98,22 @@ struct KTime {
 };
 
 struct Slot {
-  float *rgb1 = nullptr, *rgb2 = nullptr, *uv = nullptr;  // uv: dense planar 2 x H x W
+  void *rgb1 = nullptr, *rgb2 = nullptr;  // (H, W, C) fp32, or bytes when u8
+  float *uv = nullptr;                    // dense planar 2 x H x W
   int H = 0, W = 0, C = 0;
-  size_t cap_rgb = 0, cap_uv = 0;
+  bool u8 = false;
+  size_t cap_rgb = 0, cap_uv = 0;         // bytes of one frame, floats of uv
+};
+
+// of_pairs_run_host staging of one lane: two pinned input/output buffers and
+// two device frame buffers, so pair j+1's bytes go up on the copy stream and
+// pair j-1's flow comes down while pair j computes
+struct HostStage {
+  hipStream_t copy = nullptr;
+  uint8_t *pin_in[2] = {nullptr, nullptr}, *d_in[2] = {nullptr, nullptr};
+  float *pin_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_conv[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+  size_t cap_in = 0, cap_out = 0;
 };
 
 }  // namespace
@@ -158,6 +171,7 @@ struct of_ctx {
   std::map<int64_t, int> iter_hints;  // (H, W, solver) -> last iteration count
   double cur_px = 0;  // pixels processed by the launches being issued (profiling)
   std::vector<Slot> slots;
+  HostStage *hs = nullptr;      // of_pairs_run_host staging (lazily created)
   std::vector<of_ctx *> lanes;  // of_pairs_run pipelines: own stream, arena and solver state
   std::mutex big_own;           // (parent) the big-phase token its lanes share
   std::mutex *big = nullptr;    // (lane) token held through phases of >= big_px pixels
@@ -1185,7 +1199,8 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
 }
 
 // estimate_flow preprocessing (interface.py:41-64): host or device RGB input
-void estimate_dev(of_ctx *c, of_params *P, const float *rgb1, const float *rgb2, int H, int W, int C, F2 &uv,
+// rgb1/rgb2: (H, W, C) frames on the device, fp32 or (u8) bytes
+void estimate_dev(of_ctx *c, of_params *P, const void *rgb1, const void *rgb2, bool u8, int H, int W, int C, F2 &uv,
                   of_stats *st) {
   REQUIRE(C == 1 || C == 3, OF_EINVAL, "images must be (H,W) or (H,W,3)");
   hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
@@ -1196,13 +1211,19 @@ void estimate_dev(of_ctx *c, of_params *P, const float *rgb1, const float *rgb2,
   if (guide_mode) guide = new_img(c, H, W, C == 3 ? 3 : 1);
   uint32_t *mm = c->d_mm + 2 * 8;
   launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
-  if (C == 3) {
-    const long n = (long)H * W * 3;
-    launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<long>((n + 255) / 256, 256)), dim3(256), 0, rgb1, n, mm);
-  }
+  const dim3 mg((unsigned)std::min<long>(((long)H * W * 3 + 255) / 256, 256));
+  if (C == 3 && u8)
+    launch(c, "rgb_max", k_rgb_max<uint8_t>, mg, dim3(256), 0, (const uint8_t *)rgb1, (long)H * W * 3, mm);
+  else if (C == 3)
+    launch(c, "rgb_max", k_rgb_max<float>, mg, dim3(256), 0, (const float *)rgb1, (long)H * W * 3, mm);
   Grid2 g = grid2(H, W);
-  launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, rgb1, rgb2, H, W, C, gray.p, gray.P, gray.ps(),
-         guide_mode ? guide.p : (float *)nullptr, (const uint32_t *)mm);
+  float *gp = guide_mode ? guide.p : (float *)nullptr;
+  if (u8)
+    launch(c, "rgb_prep", k_rgb_prep<uint8_t>, g.grid, g.block, 0, (const uint8_t *)rgb1, (const uint8_t *)rgb2, H, W,
+           C, gray.p, gray.P, gray.ps(), gp, (const uint32_t *)mm);
+  else
+    launch(c, "rgb_prep", k_rgb_prep<float>, g.grid, g.block, 0, (const float *)rgb1, (const float *)rgb2, H, W, C,
+           gray.p, gray.P, gray.ps(), gp, (const uint32_t *)mm);
   if (guide_mode && C == 3)
     for (int ch = 0; ch < 3; ++ch) scale_img(c, view(guide, ch, 1), 0.0f, 255.0f, 9 + ch);
   HIPCHK(hipEventRecord(t1, c->stream));
@@ -1220,7 +1241,7 @@ void run_slot(of_ctx *c, const Slot &s, of_params *P, of_stats *st) {
   auto wall0 = std::chrono::steady_clock::now();
   F2 uv = new_f2(c, s.H, s.W);
   fill_f2(c, uv, 0.0f);
-  estimate_dev(c, P, s.rgb1, s.rgb2, s.H, s.W, s.C, uv, st);
+  estimate_dev(c, P, s.rgb1, s.rgb2, s.u8, s.H, s.W, s.C, uv, st);
   f2_to_dense(c, uv, s.uv);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (st)
@@ -1233,6 +1254,8 @@ int fail(of_ctx *c, const OfError &e) {
 }
 
 thread_local std::string g_err;
+
+void stage_free(of_ctx *l);
 
 }  // namespace
 
@@ -1314,6 +1337,7 @@ int of_ctx_destroy(of_ctx *c) {
   c->lanes.clear();
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  stage_free(c);
   if (c->comm) ncclCommDestroy(c->comm);
   c->arena.release();
   for (auto &s : c->slots) {
@@ -1439,7 +1463,7 @@ int of_estimate_flow(of_ctx *c, of_params *P, const float *im1, const float *im2
   HIPCHK(hipMemcpyAsync(d2, im2, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
   F2 uv = init_uv ? upload_f2(c, init_uv, H, W) : new_f2(c, H, W);
   if (!init_uv) fill_f2(c, uv, 0.0f);
-  estimate_dev(c, P, d1, d2, H, W, C, uv, st);
+  estimate_dev(c, P, d1, d2, false, H, W, C, uv, st);
   download_f2(c, uv, out_uv);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (st)
@@ -1498,12 +1522,12 @@ int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int 
   REQUIRE(slot >= 0 && slot < 4096 && im1 && im2 && (C == 1 || C == 3), OF_EINVAL, "bad arguments");
   if ((int)c->slots.size() <= slot) c->slots.resize(slot + 1);
   Slot &s = c->slots[slot];
-  const size_t n = (size_t)H * W * C, nu = 2 * (size_t)H * W;
+  const size_t n = (size_t)H * W * C * sizeof(float), nu = 2 * (size_t)H * W;
   if (s.cap_rgb < n) {
     hipFree(s.rgb1);
     hipFree(s.rgb2);
-    HIPCHK(hipMalloc(&s.rgb1, sizeof(float) * n));
-    HIPCHK(hipMalloc(&s.rgb2, sizeof(float) * n));
+    HIPCHK(hipMalloc(&s.rgb1, n));
+    HIPCHK(hipMalloc(&s.rgb2, n));
     s.cap_rgb = n;
   }
   if (s.cap_uv < nu) {
@@ -1514,8 +1538,9 @@ int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int 
   s.H = H;
   s.W = W;
   s.C = C;
-  HIPCHK(hipMemcpyAsync(s.rgb1, im1, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(s.rgb2, im2, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  s.u8 = false;
+  HIPCHK(hipMemcpyAsync(s.rgb1, im1, n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(s.rgb2, im2, n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   API_END(c)
 }
@@ -1593,6 +1618,209 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
     for (auto &t : th) t.join();
     c->big = nullptr;
     for (int li = 1; li < lanes; ++li) {  // profiling: lane timings into the ctx's table
+      for (auto &kv : c->lanes[li - 1]->ktimes) {
+        KTime &d = c->ktimes[kv.first];
+        d.ms += kv.second.ms;
+        d.px += kv.second.px;
+        d.n += kv.second.n;
+      }
+      c->lanes[li - 1]->ktimes.clear();
+    }
+    for (auto &e : errs)
+      if (e.code != OF_OK) throw e;
+  }
+  API_END(c)
+}
+
+namespace {
+void stage_alloc(of_ctx *l, size_t in_bytes, size_t out_floats) {
+  if (!l->hs) {
+    l->hs = new HostStage();
+    HIPCHK(hipStreamCreateWithFlags(&l->hs->copy, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      HIPCHK(hipEventCreateWithFlags(&l->hs->ev_in[b], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&l->hs->ev_conv[b], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&l->hs->ev_out[b], hipEventDisableTiming));
+    }
+  }
+  HostStage &h = *l->hs;
+  if (h.cap_in < in_bytes) {
+    for (int b = 0; b < 2; ++b) {
+      HIPCHK(hipEventSynchronize(h.ev_in[b]));
+      HIPCHK(hipEventSynchronize(h.ev_conv[b]));
+      if (h.pin_in[b]) hipHostFree(h.pin_in[b]);
+      hipFree(h.d_in[b]);
+      HIPCHK(hipHostMalloc((void **)&h.pin_in[b], in_bytes, hipHostMallocDefault));
+      HIPCHK(hipMalloc((void **)&h.d_in[b], in_bytes));
+    }
+    h.cap_in = in_bytes;
+  }
+  if (h.cap_out < out_floats) {
+    for (int b = 0; b < 2; ++b) {
+      HIPCHK(hipEventSynchronize(h.ev_out[b]));
+      if (h.pin_out[b]) hipHostFree(h.pin_out[b]);
+      HIPCHK(hipHostMalloc((void **)&h.pin_out[b], sizeof(float) * out_floats, hipHostMallocDefault));
+    }
+    h.cap_out = out_floats;
+  }
+}
+
+void stage_free(of_ctx *l) {
+  if (!l->hs) return;
+  HostStage &h = *l->hs;
+  if (h.copy) hipStreamSynchronize(h.copy);
+  for (int b = 0; b < 2; ++b) {
+    if (h.pin_in[b]) hipHostFree(h.pin_in[b]);
+    if (h.pin_out[b]) hipHostFree(h.pin_out[b]);
+    hipFree(h.d_in[b]);
+    for (hipEvent_t e : {h.ev_in[b], h.ev_conv[b], h.ev_out[b]})
+      if (e) hipEventDestroy(e);
+  }
+  if (h.copy) hipStreamDestroy(h.copy);
+  delete l->hs;
+  l->hs = nullptr;
+}
+
+// One lane's share of of_pairs_run_host: pairs k = first, first + step, ...
+// Per pair j (buffer b = j & 1): host bytes -> pinned -> device on the copy
+// stream (issued while pair j-1 computes), estimate_flow on the lane stream
+// straight from the bytes, flow -> slot k's device buffer (kept for the RCCL
+// gather) -> pinned on the copy stream -> caller's buffer (while pair j+1
+// computes).
+void run_host_lane(of_ctx *c, of_ctx *l, int first, int step, int npairs, const uint8_t *const *im1,
+                   const uint8_t *const *im2, int H, int W, int C, const of_params *P, float *const *out_uv,
+                   of_stats *st) {
+  HostStage &h = *l->hs;
+  const size_t nb = (size_t)H * W * C, nu = 2 * (size_t)H * W;
+  std::vector<int> ks;
+  for (int k = first; k < npairs; k += step) ks.push_back(k);
+  auto prefetch = [&](int j) {
+    const int b = j & 1, k = ks[j];
+    HIPCHK(hipEventSynchronize(h.ev_in[b]));  // pinned buffer b free (its last H2D done)
+    memcpy(h.pin_in[b], im1[k], nb);
+    memcpy(h.pin_in[b] + nb, im2[k], nb);
+    HIPCHK(hipStreamWaitEvent(h.copy, h.ev_conv[b], 0));  // device buffer b no longer read
+    HIPCHK(hipMemcpyAsync(h.d_in[b], h.pin_in[b], 2 * nb, hipMemcpyHostToDevice, h.copy));
+    HIPCHK(hipEventRecord(h.ev_in[b], h.copy));
+  };
+  auto finish = [&](int j) {
+    const int b = j & 1;
+    HIPCHK(hipEventSynchronize(h.ev_out[b]));
+    memcpy(out_uv[ks[j]], h.pin_out[b], sizeof(float) * nu);
+  };
+  // the host copies of pair j+1 (in) and pair j-1 (out) run on a helper
+  // thread while this thread drives pair j's kernels
+  std::thread io;
+  OfError io_err{OF_OK, ""};
+  auto join_io = [&] {
+    if (io.joinable()) io.join();
+    if (io_err.code != OF_OK) throw io_err;
+  };
+  if (!ks.empty()) prefetch(0);
+  for (int j = 0; j < (int)ks.size(); ++j) {
+    const int b = j & 1, k = ks[j];
+    join_io();
+    l->arena.reset();
+    l->tev_used = 0;
+    HIPCHK(hipStreamWaitEvent(l->stream, h.ev_in[b], 0));
+    Slot s;
+    s.rgb1 = h.d_in[b];
+    s.rgb2 = h.d_in[b] + nb;
+    s.u8 = true;
+    s.uv = c->slots[k].uv;
+    s.H = H;
+    s.W = W;
+    s.C = C;
+    io = std::thread([&, j] {
+      try {
+        HIPCHK(hipSetDevice(l->device));
+        if (j + 1 < (int)ks.size()) prefetch(j + 1);
+        if (j) finish(j - 1);
+      } catch (const OfError &e) {
+        io_err = e;
+      }
+    });
+    try {
+      of_params Pc = *P;
+      run_slot(l, s, &Pc, k == 0 ? st : nullptr);
+    } catch (...) {
+      if (io.joinable()) io.join();
+      throw;
+    }
+    HIPCHK(hipEventRecord(h.ev_conv[b], l->stream));  // frames of buffer b consumed, flow k complete
+    HIPCHK(hipStreamWaitEvent(h.copy, h.ev_conv[b], 0));
+    HIPCHK(hipMemcpyAsync(h.pin_out[b], s.uv, sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
+    HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
+  }
+  join_io();
+  if (!ks.empty()) finish((int)ks.size() - 1);
+  HIPCHK(hipStreamSynchronize(h.copy));
+}
+}  // namespace
+
+// Host-to-host batch (SURVEY.md §8d headline: wall clock including the H2D of
+// the uint8 pair and the D2H of uv): pairs are read from caller-owned (H, W, C)
+// uint8 frames and the flows written to caller-owned planar 2 x H x W fp32
+// buffers, `lanes` pairs in flight as in of_pairs_run.  Slots 0..npairs-1 keep
+// each pair's flow on the device afterwards (of_rccl_gather_flows,
+// of_pair_download).
+int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const uint8_t *const *im2, int H, int W,
+                      int C, const of_params *P, int lanes, float *const *out_uv, of_stats *st) {
+  API_BEGIN(c)
+  REQUIRE(P && im1 && im2 && out_uv && npairs >= 1 && npairs <= 4096 && H > 0 && W > 0 && (C == 1 || C == 3) &&
+              lanes >= 1 && lanes <= 16,
+          OF_EINVAL, "bad arguments");
+  for (int k = 0; k < npairs; ++k) REQUIRE(im1[k] && im2[k] && out_uv[k], OF_EINVAL, "null pair buffer");
+  if ((int)c->slots.size() < npairs) c->slots.resize(npairs);
+  const size_t nu = 2 * (size_t)H * W;
+  for (int k = 0; k < npairs; ++k) {
+    Slot &s = c->slots[k];
+    if (s.cap_uv < nu) {
+      hipFree(s.uv);
+      HIPCHK(hipMalloc(&s.uv, sizeof(float) * nu));
+      s.cap_uv = nu;
+    }
+    s.H = H;
+    s.W = W;
+    s.C = C;
+  }
+  lanes = std::min(lanes, npairs);
+  while ((int)c->lanes.size() < lanes - 1) {
+    of_ctx *l = nullptr;
+    const int rc = of_ctx_create(c->device, &l);
+    REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
+    c->lanes.push_back(l);
+  }
+  for (int li = 0; li < lanes; ++li) stage_alloc(li ? c->lanes[li - 1] : c, 2 * (size_t)H * W * C, nu);
+  if (lanes == 1) {
+    run_host_lane(c, c, 0, 1, npairs, im1, im2, H, W, C, P, out_uv, st);
+  } else {
+    std::vector<std::thread> th;
+    std::vector<OfError> errs(lanes, OfError{OF_OK, ""});
+    for (int li = 0; li < lanes; ++li) {
+      of_ctx *l = li ? c->lanes[li - 1] : c;
+      l->prof = c->prof;
+      l->big = OF_BIG_PX > 0 ? &c->big_own : nullptr;
+      l->big_px = OF_BIG_PX;
+      th.emplace_back([=, &errs] {
+        try {
+          HIPCHK(hipSetDevice(l->device));
+          run_host_lane(c, l, li, lanes, npairs, im1, im2, H, W, C, P, out_uv, st);
+          if (l != c) flush_prof(l);
+        } catch (const OfError &e) {
+          errs[li] = e;
+          hipStreamSynchronize(l->stream);
+          if (l->hs) hipStreamSynchronize(l->hs->copy);
+          l->pending.clear();
+          l->ev_used = 0;
+        } catch (const std::exception &e) {
+          errs[li] = OfError{OF_ENOMEM, e.what()};
+        }
+      });
+    }
+    for (auto &t : th) t.join();
+    c->big = nullptr;
+    for (int li = 1; li < lanes; ++li) {
       for (auto &kv : c->lanes[li - 1]->ktimes) {
         KTime &d = c->ktimes[kv.first];
         d.ms += kv.second.ms;
@@ -1686,10 +1914,10 @@ int of_preprocess(of_ctx *c, const float *rgb1, const float *rgb2, int H, int W,
   Img gray = new_img(c, H, W, 2), g3 = new_img(c, H, W, 3);
   uint32_t *mm = c->d_mm + 2 * 8;
   launch(c, "mm_init", k_mm_init, dim3(1), dim3(64), 0, mm, 1);
-  launch(c, "rgb_max", k_rgb_max, dim3((unsigned)std::min<size_t>((n + 255) / 256, 256)), dim3(256), 0,
+  launch(c, "rgb_max", k_rgb_max<float>, dim3((unsigned)std::min<size_t>((n + 255) / 256, 256)), dim3(256), 0,
          (const float *)d1, (long)n, mm);
   Grid2 g = grid2(H, W);
-  launch(c, "rgb_prep", k_rgb_prep, g.grid, g.block, 0, (const float *)d1, (const float *)d2, H, W, 3, gray.p, gray.P,
+  launch(c, "rgb_prep", k_rgb_prep<float>, g.grid, g.block, 0, (const float *)d1, (const float *)d2, H, W, 3, gray.p, gray.P,
          gray.ps(), g3.p, (const uint32_t *)mm);
   for (int ch = 0; ch < 3; ++ch) scale_img(c, view(g3, ch, 1), 0.0f, 255.0f, 9 + ch);
   download_img(c, gray, gray_pair);

@@ -60,10 +60,12 @@ __global__ void k_scale(float *__restrict__ a, int H, int W, int P, int planes, 
 
 // ---------------------------------------------------------------------------
 // colour conversion (interface.py:74-141).  rgb: interleaved H x W x C dense.
-__global__ void k_rgb_max(const float *__restrict__ rgb, long n, uint32_t *mm) {
+// T = float (caller-converted frames) or uint8_t (frames uploaded as bytes)
+template <typename TI>
+__global__ void k_rgb_max(const TI *__restrict__ rgb, long n, uint32_t *mm) {
   uint32_t hi = 0u;
   for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x)
-    hi = max(hi, f2ord(rgb[k]));
+    hi = max(hi, f2ord((float)rgb[k]));
   for (int off = 32; off > 0; off >>= 1) hi = max(hi, (uint32_t)__shfl_down((int)hi, off, 64));
   __shared__ uint32_t s_hi[4];  // 256-thread blocks: one atomic per block
   if ((threadIdx.x & 63) == 0) s_hi[threadIdx.x >> 6] = hi;
@@ -77,23 +79,25 @@ __device__ __forceinline__ float q_u8(float x) {
 }
 
 // gray (uint8 round trip) of both frames; Lab of frame 1 when lab != nullptr
-__global__ void k_rgb_prep(const float *__restrict__ rgb1, const float *__restrict__ rgb2, int H, int W, int C,
+template <typename TI>
+__global__ void k_rgb_prep(const TI *__restrict__ rgb1, const TI *__restrict__ rgb2, int H, int W, int C,
                            float *gray, int P, size_t ps, float *lab, const uint32_t *mm_rgbmax) {
   const bool norm = ord2f(mm_rgbmax[1]) > 1.0f;
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     size_t k = (size_t)i * W + j, o = (size_t)i * P + j;
     if (C == 1) {
-      gray[o] = rgb1[k];
-      gray[ps + o] = rgb2[k];
-      if (lab) lab[o] = rgb1[k];
+      gray[o] = (float)rgb1[k];
+      gray[ps + o] = (float)rgb2[k];
+      if (lab) lab[o] = (float)rgb1[k];
       continue;
     }
-    const float *a = rgb1 + 3 * k, *b = rgb2 + 3 * k;
-    gray[o] = floorf(0.2989f * q_u8(a[0]) + 0.5870f * q_u8(a[1]) + 0.1140f * q_u8(a[2]) + 0.5f);
-    gray[ps + o] = floorf(0.2989f * q_u8(b[0]) + 0.5870f * q_u8(b[1]) + 0.1140f * q_u8(b[2]) + 0.5f);
+    const TI *a = rgb1 + 3 * k, *b = rgb2 + 3 * k;
+    const float a0 = (float)a[0], a1 = (float)a[1], a2 = (float)a[2];
+    gray[o] = floorf(0.2989f * q_u8(a0) + 0.5870f * q_u8(a1) + 0.1140f * q_u8(a2) + 0.5f);
+    gray[ps + o] = floorf(0.2989f * q_u8((float)b[0]) + 0.5870f * q_u8((float)b[1]) + 0.1140f * q_u8((float)b[2]) + 0.5f);
     if (!lab) continue;
-    float R = a[0], G = a[1], B = a[2];
+    float R = a0, G = a1, B = a2;
     if (norm) { R /= 255.0f; G /= 255.0f; B /= 255.0f; }
     const float T = 0.008856f;
     float X = (0.412453f * R + 0.357580f * G + 0.180423f * B) / 0.950456f;

@@ -43,6 +43,8 @@ _SIGS = {
     "of_pair_upload": ([_vp, C.c_int, _fp, _fp, C.c_int, C.c_int, C.c_int], C.c_int),
     "of_pair_run": ([_vp, C.c_int, C.POINTER(OfParams), C.POINTER(OfStats)], C.c_int),
     "of_pairs_run": ([_vp, C.c_int, C.POINTER(OfParams), C.c_int, C.POINTER(OfStats)], C.c_int),
+    "of_pairs_run_host": ([_vp, C.c_int, C.POINTER(_vp), C.POINTER(_vp), C.c_int, C.c_int, C.c_int,
+                           C.POINTER(OfParams), C.c_int, C.POINTER(_vp), C.POINTER(OfStats)], C.c_int),
     "of_pair_download": ([_vp, C.c_int, _fp], C.c_int),
     "of_rccl_unique_id": ([C.c_char_p], C.c_int),
     "of_rccl_init": ([_vp, C.c_char_p, C.c_int, C.c_int], C.c_int),

@@ -44,6 +44,52 @@ def estimate_flow(im1, im2, method='classic+nl-fast', params=None):
     return nat.interleaved(out)
 
 
+def _as_u8(im):
+    a = np.asarray(im)
+    if a.dtype == np.uint8:
+        return np.ascontiguousarray(a)
+    f = np.asarray(a, dtype=float)
+    if not (np.all(f == np.floor(f)) and f.min() >= 0 and f.max() <= 255):
+        raise ValueError("estimate_flow_batch takes uint8 frames (or integer-valued 0..255)")
+    return np.ascontiguousarray(f.astype(np.uint8))
+
+
+def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes=2):
+    """estimate_flow over a batch of uint8 frame pairs, host to host: one C
+    call (of_pairs_run_host) keeps `lanes` pairs in flight on the GPU with
+    their uploads and downloads overlapped.  Returns a list of (H, W, 2)
+    float64 flows equal to [estimate_flow(a, b, method, params) ...]."""
+    a = [_as_u8(x) for x in im1s]
+    b = [_as_u8(x) for x in im2s]
+    if not a or len(a) != len(b):
+        raise ValueError("im1s and im2s must be non-empty and of equal length")
+    H, W = a[0].shape[:2]
+    if a[0].ndim == 3 and a[0].shape[2] < 3:
+        raise ValueError("estimate_flow_batch takes (H, W) or (H, W, >=3) frames")
+    Cc = 3 if a[0].ndim == 3 else 1
+    a = [x[:, :, :3] if x.ndim == 3 else x for x in a]
+    b = [x[:, :, :3] if x.ndim == 3 else x for x in b]
+    for x in a + b:
+        if x.shape[:2] != (H, W) or (x.ndim == 3) != (Cc == 3):
+            raise ValueError("all frames of a batch must share one shape")
+    a = [np.ascontiguousarray(x) for x in a]
+    b = [np.ascontiguousarray(x) for x in b]
+    ope = load_of_method(method)
+    if params is not None:
+        ope.parse_input_parameter(params)
+    P = ope.to_params()
+    P.guide_mode = int(ope._METHOD == 'classic_nl' and ope.color_images is not None)
+    n = len(a)
+    outs = [np.empty((2, H, W), dtype=np.float32) for _ in range(n)]
+    vp = C.c_void_p
+    p1 = (vp * n)(*[x.ctypes.data for x in a])
+    p2 = (vp * n)(*[x.ctypes.data for x in b])
+    po = (vp * n)(*[o.ctypes.data for o in outs])
+    ctx = nat.context()
+    ctx.check(ctx.lib.of_pairs_run_host(ctx.handle, n, p1, p2, H, W, Cc, C.byref(P), int(lanes), po, None))
+    return [nat.interleaved(o) for o in outs]
+
+
 def _preprocess(im1, im2):
     a = nat.f32(np.asarray(im1, dtype=float)[:, :, :3])
     b = nat.f32(np.asarray(im2, dtype=float)[:, :, :3])

@@ -101,3 +101,44 @@ def test_roofline_of_all_and_finest():
     assert r["mean_launch_ms"] == pytest.approx(3.0 / 20, rel=1e-3)
     assert r["finest"]["mean_launch_ms"] == pytest.approx(2.0 / 10, rel=1e-3)
     assert r["finest"]["mean_active_launch_ms"] == pytest.approx(2.0 / 8, rel=1e-3)
+
+
+def _gather_worker(rank, world, port, pairs, q):
+    """bench.gather_check's digest exchange and layout verification over
+    gloo; the device gather itself (of_rccl_gather_flows: rank 0 receives
+    rank src's slot s at src * P + s) is emulated with gather_object."""
+    import numpy as np
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    dist, w, r, _ = bench.dist_setup(None)
+    outs = [np.random.default_rng(k).random((2, 6, 5)).astype(np.float32) for k in bench.shard_seeds(r, pairs)]
+    every = [None] * w
+    dist.all_gather_object(every, bench.flow_digests(outs))
+    got = [None] * w if r == 0 else None
+    dist.gather_object(outs, got, dst=0)
+    res = None
+    if r == 0:
+        buf = np.stack([got[src][s] for src in range(w) for s in range(pairs)])
+        ok = bench.verify_gather(buf, every, w, pairs)
+        bad = buf.copy()
+        bad[[0, -1]] = bad[[-1, 0]]  # two pairs swapped: must be caught
+        res = (ok, bench.verify_gather(bad, every, w, pairs))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_layout_check_world2():
+    world, pairs = 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, pairs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == (True, False)

@@ -110,3 +110,28 @@ def test_rccl_gather_single_rank():
     finally:
         lib.of_rccl_finalize(ctx.handle)
         ctx.close()
+
+
+@pytest.mark.parametrize("lanes,n,H,W", [(1, 3, 60, 88), (2, 5, 60, 88), (3, 4, 270, 480)])
+def test_pairs_run_host_matches_estimate_flow(lanes, n, H, W):
+    """of_pairs_run_host (uint8 frames in host memory -> flows in host
+    memory, uploads/downloads overlapped on copy streams) equals
+    estimate_flow on every pair bitwise (same kernels; the bytes path
+    computes gray/Lab from the same integer values), for any lane count;
+    the flows also stay in device slots 0..n-1."""
+    import optical_flow
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    pairs = [synth_pair(H, W, 10 + k) for k in range(n)]
+    a = [p[0].astype(np.uint8) for p in pairs]
+    b = [p[1].astype(np.uint8) for p in pairs]
+    got = optical_flow.estimate_flow_batch(a, b, "classic+nl-fast", lanes=lanes)
+    for k in range(n):
+        ref = optical_flow.estimate_flow(pairs[k][0], pairs[k][1], "classic+nl-fast")
+        assert np.array_equal(got[k], ref), (k, np.abs(got[k] - ref).max())
+    ctx = _native.context()
+    uv = np.empty((2, H, W), np.float32)
+    ctx.check(ctx.lib.of_pair_download(ctx.handle, n - 1, _native.ptr(uv)))
+    assert np.array_equal(np.moveaxis(uv, 0, 2), got[n - 1])
+    with pytest.raises(ValueError):
+        optical_flow.estimate_flow_batch([a[0] + 0.5], [b[0]])

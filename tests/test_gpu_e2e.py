@@ -19,16 +19,19 @@ def _aepe(uv, gt):
     return float(np.sqrt(((uv - gt) ** 2).sum(-1)).mean())
 
 
-# Tolerances per method family, from measurement (DESIGN.md "Parity"):
-#  - stable (HS, BA-Lorentzian): float32 vs float64 only;
-#  - Classic+NL: weighted median over 225 samples (fp32 weights may pick a
-#    neighbouring order statistic);
-#  - charbonnier (classic-c*, classic++): chaotic in the reference itself -
-#    perturbing its direct solve by 1e-12 (relative) moves its own output by
-#    4.7e-3 / 5.4e-3 px mean on this crop;
+# Tolerances per method family: about 3-8x the mean / median EPE to the
+# reference measured on the GPU (round 2, profiles/r2j_*; the kernels are
+# deterministic, so a rerun reproduces those numbers exactly):
+#  - stable (HS, BA-Lorentzian): float32 vs float64 only (<= 2.6e-6 / 1.3e-6);
+#  - nlfast (Classic+NL-fast): 2.9e-5 / 4.4e-6 on the crop, 1.8e-4 / 1.2e-5 on
+#    the synthetic pair (the weighted median amplifies single-pixel flips);
+#  - nl (Classic+NL, gnc 3 with the 0.5 blend): 2.9e-3 / 4.0e-4;
+#  - chaotic (classic-c*, classic++): the reference itself moves by
+#    4.7e-3 / 5.4e-3 px mean when its direct solve is perturbed by 1e-12
+#    (relative); measured 1.2e-2 / 6.5e-3 at most;
 #  - classic-c-a: the reference diverges (|uv| ~ 3.6e36); so must we.
-TOL = {"stable": (1e-3, 2e-4), "nl": (1e-2, 2e-3), "chaotic": (3e-2, 2e-2)}
-FAMILY = {"classic+nl-fast": "nl", "classic+nl": "nl", "classic+nl-full": "nl", "hs-brightness": "stable",
+TOL = {"stable": (2e-5, 1e-5), "nlfast": (5e-4, 4e-5), "nl": (1e-2, 2e-3), "chaotic": (3e-2, 2e-2)}
+FAMILY = {"classic+nl-fast": "nlfast", "classic+nl": "nl", "classic+nl-full": "nl", "hs-brightness": "stable",
           "hs": "stable", "ba-brightness": "stable", "ba": "stable", "classic-l": "stable",
           "classic-c-brightness": "chaotic", "classic-c": "chaotic", "classic++": "chaotic"}
 
@@ -70,7 +73,7 @@ def test_e2e_synthetic(golden, method):
     s = epe_stats(uv, d[method])
     da = abs(_aepe(uv, d["gt"]) - _aepe(d[method], d["gt"]))
     print(method, s, "dAEPE", da)
-    fam = {"classic+nl-fast": "nl", "hs": "stable", "hs-brightness": "stable", "classic-c": "chaotic"}[method]
+    fam = FAMILY[method]
     mean_tol, med_tol = TOL[fam]
     assert s["mean"] < mean_tol and s["median"] < med_tol, s
     assert da < (3e-3 if fam == "chaotic" else 1e-3)
