@@ -220,6 +220,72 @@ def roofline_of(ktimes, per_level):
     return out
 
 
+def profiled_replay(ctx, lib, P0, pairs, lanes):
+    """One step of of_pairs_run with per-launch HIP-event timing keyed by
+    kernel and level size; returns (per-kernel totals, per-(kernel, px))."""
+    ctx.check(lib.of_set_profiling(ctx.handle, 2))
+    run_step(ctx, P0, pairs, lanes)
+    n = C.c_int(0)
+    names = (C.c_char_p * 1024)()
+    ms = (C.c_double * 1024)()
+    cnt = (C.c_int64 * 1024)()
+    pxs = (C.c_double * 1024)()
+    ctx.check(lib.of_kernel_times(ctx.handle, 1024, names, ms, cnt, pxs, C.byref(n)))
+    ctx.check(lib.of_set_profiling(ctx.handle, 0))
+    per_level, ktimes = {}, {}
+    for i in range(min(n.value, 1024)):
+        name, lvl = names[i].decode().rsplit("@", 1)
+        rec = {"ms_total": ms[i], "launches": int(cnt[i]), "px": pxs[i]}
+        per_level[(name, int(lvl))] = rec
+        agg = ktimes.setdefault(name, {"ms_total": 0.0, "launches": 0.0, "px": 0.0})
+        for k in agg:
+            agg[k] += rec[k]
+    return ktimes, per_level
+
+
+# SURVEY.md §8d inner-loop figure ("SOR/PCG + warp"): per warping iteration
+# N (48 warp+derivatives + 56 weights/assembly + 24 update/clip) + 76 N K_pcg
+# bytes, over the time of every kernel of the loop
+INNER_BYTES = {"partial_deriv_hermite": 48, "partial_deriv_bspline": 44, "partial_deriv_bilinear": 44,
+               "flow_operator": 56, "update_occ": 24}
+INNER_TIME_ONLY = ("pcg_small", "pcg_check", "axpy_diff", "add_update", "sor_sweep")
+
+
+def inner_loop_of(ktimes, per_level):
+    """bytes: the per-px figures above x the pixels of every launch, and
+    76 B x the pixels of every CG launch that did work (pcg_iter.active;
+    the one-workgroup coarse-level solves, pcg_small, count time but no
+    bytes: conservative); time: HIP events of all those kernels."""
+    byt, ms = 0.0, 0.0
+    for name, rec in ktimes.items():
+        if name in INNER_BYTES:
+            byt += INNER_BYTES[name] * rec["px"]
+            ms += rec["ms_total"]
+        elif name == "pcg_iter":
+            ms += rec["ms_total"]
+        elif name in INNER_TIME_ONLY:
+            ms += rec["ms_total"]
+    act = ktimes.get("pcg_iter.active")
+    if act:
+        byt += KERNEL_BYTES_PER_PX["pcg_iter"] * act["px"]
+    if ms <= 0:
+        return None
+    ach = byt / (ms * 1e-3) / 1e9
+    fine = max((px for (n, px) in per_level if n == "pcg_iter"), default=None)
+    out = {"bytes_per_step": round(byt), "kernel_ms_per_step": round(ms, 3), "achieved": round(ach, 1),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+           "formula": "sum N*(48+56+24) per warp + 76*N*K_pcg; time of warp, assembly, update, CG kernels"}
+    if fine:
+        b2 = sum(INNER_BYTES[n] * r["px"] for (n, px), r in per_level.items() if px == fine and n in INNER_BYTES)
+        b2 += KERNEL_BYTES_PER_PX["pcg_iter"] * per_level.get(("pcg_iter.active", fine), {"px": 0})["px"]
+        m2 = sum(r["ms_total"] for (n, px), r in per_level.items() if px == fine and
+                 (n in INNER_BYTES or n == "pcg_iter" or n in INNER_TIME_ONLY))
+        if m2 > 0:
+            a2 = b2 / (m2 * 1e-3) / 1e9
+            out["finest"] = {"px": fine, "achieved": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4)}
+    return out
+
+
 def main():
     args = parse()
     dist, world, rank, local = dist_setup(args)
@@ -299,32 +365,22 @@ def main():
     roofline = None
     ktimes = {}
     pcg_levels = None
+    inner = None
     if not args.no_profile:
         # profiled replay of one step, same pairs and lanes as the timed
         # steps: HIP events around every launch on the stream it runs on
-        rsteps = 1
-        ctx.check(lib.of_set_profiling(ctx.handle, 2))  # keyed by kernel and level size
-        for _ in range(rsteps):
-            run_step(ctx, P0, args.pairs, args.lanes)
-        n = C.c_int(0)
-        names = (C.c_char_p * 1024)()
-        ms = (C.c_double * 1024)()
-        cnt = (C.c_int64 * 1024)()
-        pxs = (C.c_double * 1024)()
-        ctx.check(lib.of_kernel_times(ctx.handle, 1024, names, ms, cnt, pxs, C.byref(n)))
-        ctx.check(lib.of_set_profiling(ctx.handle, 0))
-        per_level = {}
-        for i in range(min(n.value, 1024)):
-            name, lvl = names[i].decode().rsplit("@", 1)
-            rec = {"ms_total": ms[i] / rsteps, "launches": int(cnt[i]) / rsteps, "px": pxs[i] / rsteps}
-            per_level[(name, int(lvl))] = rec
-            agg = ktimes.setdefault(name, {"ms_total": 0.0, "launches": 0.0, "px": 0.0})
-            for k in agg:
-                agg[k] += rec[k]
+        ktimes, per_level = profiled_replay(ctx, lib, P0, args.pairs, args.lanes)
         roofline = roofline_of(ktimes, per_level)
         pcg_levels = [{"px": px, "ms": round(rec["ms_total"] / args.pairs, 3), "launches": rec["launches"] / args.pairs,
                        "active": per_level.get(("pcg_iter.active", px), {}).get("launches", 0) / args.pairs}
                       for (n, px), rec in sorted(per_level.items(), key=lambda kv: -kv[0][1]) if n == "pcg_iter"]
+        inner = inner_loop_of(ktimes, per_level)
+        # the same pairs one at a time (lanes = 1): kernel durations without a
+        # second pipeline's kernels sharing the CUs
+        kt1, pl1 = profiled_replay(ctx, lib, P0, args.pairs, 1)
+        inner["isolated"] = inner_loop_of(kt1, pl1)
+        if roofline is not None:
+            roofline["inner_loop"] = inner
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)

@@ -177,6 +177,13 @@ int of_compute_flow(of_ctx *ctx, of_params *params, const float *images, int H, 
  * classic_nl.py:200-277).  uv_in / out_uv planar 2 x H x W. */
 int of_compute_flow_base(of_ctx *ctx, of_params *params, const float *images, int H, int W, int nc,
                          const float *guide, int gc, double alpha, const float *uv_in, float *out_uv);
+/* AltBAOpticalFlow.compute_flow_base(uv, uvhat) (alt_ba.py:189-274): one
+ * level of the coupled IRLS (lambda2 annealed 1e-4 -> lambda2 over max_iters
+ * warps, coupling weights rho_couple'(uv - uvhat)/x, Li-Osher median update
+ * of uvhat, uv <- uvhat when `replacement`); uv, uvhat in and out are planar
+ * 2 x H x W */
+int of_alt_ba_flow_base(of_ctx *ctx, of_params *params, const float *images, int H, int W, int nc, double alpha,
+                        int replacement, const float *uv, const float *uvhat, float *out_uv, float *out_uvhat);
 
 /* ---- device-resident batch path (benchmark / multi-GPU sharding) ---- */
 /* upload one RGB/gray pair into slot `slot` of the ctx (H2D, untimed) */

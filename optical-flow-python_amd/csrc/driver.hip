@@ -1516,6 +1516,28 @@ int of_compute_flow_base(of_ctx *c, of_params *P, const float *images, int H, in
   API_END(c)
 }
 
+// AltBAOpticalFlow.compute_flow_base(uv, uvhat) (alt_ba.py:189-274): one
+// pyramid level of the coupled IRLS with lambda2 annealing and the Li-Osher
+// median update of uvhat; returns both fields
+int of_alt_ba_flow_base(of_ctx *c, of_params *P, const float *images, int H, int W, int nc, double alpha,
+                        int replacement, const float *uv_in, const float *uvhat_in, float *out_uv,
+                        float *out_uvhat) {
+  API_BEGIN(c)
+  REQUIRE(P && images && uv_in && uvhat_in && out_uv && out_uvhat && H > 0 && W > 0 && nc >= 1, OF_EINVAL,
+          "bad arguments");
+  REQUIRE(P->method == OF_METHOD_ALT_BA, OF_EINVAL, "of_alt_ba_flow_base needs an AltBA parameter set");
+  check_params(P);
+  LevelIn L;
+  L.im = new_img(c, H, W, 2 * nc);
+  upload_img(c, L.im, images);
+  F2 uv = upload_f2(c, uv_in, H, W), uvhat = upload_f2(c, uvhat_in, H, W);
+  altba_base(c, P, L, uv, uvhat, alpha, replacement != 0, nullptr);
+  download_f2(c, uv, out_uv);
+  download_f2(c, uvhat, out_uvhat);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
 // ---- device-resident slots ----
 int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int H, int W, int C) {
   API_BEGIN(c)

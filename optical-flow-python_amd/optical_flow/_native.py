@@ -40,6 +40,8 @@ _SIGS = {
                          C.POINTER(OfStats)], C.c_int),
     "of_compute_flow_base": ([_vp, C.POINTER(OfParams), _fp, C.c_int, C.c_int, C.c_int, _fp, C.c_int,
                               C.c_double, _fp, _fp], C.c_int),
+    "of_alt_ba_flow_base": ([_vp, C.POINTER(OfParams), _fp, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, _fp,
+                             _fp, _fp, _fp], C.c_int),
     "of_pair_upload": ([_vp, C.c_int, _fp, _fp, C.c_int, C.c_int, C.c_int], C.c_int),
     "of_pair_run": ([_vp, C.c_int, C.POINTER(OfParams), C.POINTER(OfStats)], C.c_int),
     "of_pairs_run": ([_vp, C.c_int, C.POINTER(OfParams), C.c_int, C.POINTER(OfStats)], C.c_int),

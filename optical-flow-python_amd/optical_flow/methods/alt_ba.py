@@ -1,8 +1,11 @@
 """Alternative BA with auxiliary flow + Li-Osher median
 (reference: optical_flow/methods/alt_ba.py:28-372)."""
+import ctypes as C
+
 import numpy as np
 
 from optical_flow import _abi
+from optical_flow import _native as nat
 from optical_flow.methods.base import BaseOpticalFlow
 from optical_flow.robust.robust_function import RobustFunction
 
@@ -56,5 +59,16 @@ class AltBAOpticalFlow(BaseOpticalFlow):
         one = _abi.penalty('quadratic', 1.0)
         return one, [one, one], [one, one]
 
-    def compute_flow_base(self, uv, uvhat=None):
-        raise NotImplementedError("AltBA compute_flow_base(uv, uvhat) is only available through compute_flow")
+    def compute_flow_base(self, uv, uvhat):
+        """One pyramid level with coupling and Li-Osher denoising
+        (alt_ba.py:189-274) on self.images with self.alpha and
+        self.replacement; returns (uv, uvhat)."""
+        images, H, W, nc = self._images_planar()
+        P = self.to_params()
+        out_uv = np.empty((2, H, W), dtype=np.float32)
+        out_hat = np.empty((2, H, W), dtype=np.float32)
+        ctx = nat.context()
+        ctx.check(ctx.lib.of_alt_ba_flow_base(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc, float(self.alpha),
+                                              int(bool(self.replacement)), nat.ptr(nat.planar(uv)),
+                                              nat.ptr(nat.planar(uvhat)), nat.ptr(out_uv), nat.ptr(out_hat)))
+        return nat.interleaved(out_uv), nat.interleaved(out_hat)

@@ -934,6 +934,15 @@ static void altba_base(drv_t *d, const level_t *L, double *uv, double *uvhat, do
   free(It); free(Ix); free(Iy); free(coef); free(rhs); free(x); free(duv); free(l2s);
 }
 
+/* AltBAOpticalFlow.compute_flow_base(uv, uvhat) on one level (alt_ba.py:189-274);
+ * images planar 2*nc, uv and uvhat planar 2 x H x W, updated in place */
+void ofr_alt_ba_flow_base(const of_params *P, const double *images, int H, int W, int nc, double alpha,
+                          int replacement, double *uv, double *uvhat) {
+  drv_t d = {P, NULL, nc, 0};
+  level_t L = {H, W, (double *)images, NULL};
+  altba_base(&d, &L, uv, uvhat, alpha, replacement);
+}
+
 /* compute_flow for all four methods.  images planar 2*nc (frame-1 channels
  * then frame-2 channels); guide planar gc or NULL; init_uv may be NULL.
  * P->alpha is updated to the final GNC alpha (restored for BA). */

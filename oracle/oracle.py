@@ -39,6 +39,8 @@ def lib():
                                            C.POINTER(_abi.OfStats)]
         _lib.ofr_flow_operator.argtypes = [C.POINTER(_abi.OfParams), C.c_double, _dp, _dp, _dp, _dp, _dp, C.c_int,
                                            C.c_int, C.c_int, _dp, _dp]
+        _lib.ofr_alt_ba_flow_base.argtypes = [C.POINTER(_abi.OfParams), _dp, C.c_int, C.c_int, C.c_int, C.c_double,
+                                              C.c_int, _dp, _dp]
         _lib.ofr_solve.argtypes = [C.POINTER(_abi.OfParams), _dp, _dp, C.c_int, C.c_int, _dp, _ip, _dp]
         _lib.ofr_num_threads.restype = C.c_int
     return _lib
@@ -236,6 +238,18 @@ def compute_flow(ope, init=None):
                            _p(None if init is None else planar(init)), _p(out), C.byref(st))
     ope.alpha = P.alpha
     return unplanar(out, False), st
+
+
+def alt_ba_flow_base(ope, uv, uvhat):
+    """AltBAOpticalFlow.compute_flow_base(uv, uvhat) (alt_ba.py:189-274) with
+    ope's attribute bag, ope.alpha and ope.replacement."""
+    P = ope.to_params()
+    im = planar(ope.images)
+    H, W = im.shape[1:]
+    u, uh = planar(uv).copy(), planar(uvhat).copy()
+    lib().ofr_alt_ba_flow_base(C.byref(P), _p(im), H, W, im.shape[0] // 2, C.c_double(float(ope.alpha)),
+                               int(bool(ope.replacement)), _p(u), _p(uh))
+    return unplanar(u, False), unplanar(uh, False)
 
 
 def estimate_flow(im1, im2, method='classic+nl-fast', params=None, solver=None):

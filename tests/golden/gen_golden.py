@@ -334,6 +334,46 @@ def gen_full480sor():
     _full("ref480_hs_sor_sub2.npz", 480, 640, "hs", {"solver": "sor"}, 2)
 
 
+def gen_altba():
+    """AltBA (classic-c-a) parity vectors.  The registry's classic-c-a
+    diverges in the reference (|uv| ~ 3.6e36 on the crop); lambda2 = 0.01
+    converges, so the end-to-end vector uses it.  Plus single-level
+    compute_flow_base(uv, uvhat) outputs (alt_ba.py:189-274) and denoise_LO
+    (denoising.py:6-30) on a smooth random field."""
+    from optical_flow.utils.denoising import denoise_LO
+    im1, im2 = rubberwhale()
+    c1 = im1[150:198, 250:314].copy()
+    c2 = im2[150:198, 250:314].copy()
+    out = {"im1": c1, "im2": c2}
+    out["e2e_lam2_0.01"] = quiet(ref.estimate_flow, c1, c2, "classic-c-a", {"lambda2": 0.01})
+    # compute_flow_base on one level: gray pair scaled to [0, 255]
+    g = np.stack([ref_iface._rgb2gray(c1), ref_iface._rgb2gray(c2)], axis=2)
+    g = ref_ip.scale_image(g, 0, 255)
+    rng = np.random.default_rng(17)
+    H, W = g.shape[:2]
+    yy, xx = np.mgrid[0:H, 0:W]
+    uv0 = np.stack([0.6 * np.sin(xx / 9.0) + 0.2, 0.4 * np.cos(yy / 7.0) - 0.1], axis=2)
+    uvh0 = uv0 + 0.05 * rng.standard_normal(uv0.shape)
+    out["base_images"], out["base_uv"], out["base_uvhat"] = g, uv0, uvh0
+    for alpha in (1.0, 0.0):
+        for rep in (True, False):
+            o = ref_cfg.load_of_method("classic-c-a")
+            o.images = g
+            o.lambda2 = 0.01
+            o.max_iters = 4
+            o.alpha = alpha
+            o.replacement = rep
+            u, uh = quiet(o.compute_flow_base, uv0.copy(), uvh0.copy())
+            out[f"base_a{int(alpha)}_r{int(rep)}_uv"] = u
+            out[f"base_a{int(alpha)}_r{int(rep)}_uvhat"] = uh
+    # denoise_LO on a smooth field + noise
+    un = np.sin(xx[:37, :53] / 5.0) + 0.3 * rng.standard_normal((37, 53))
+    out["lo_un"] = un
+    for tag, (sz, lam, it) in {"5_0.3_1": ([5, 5], 0.3, 1), "5_0.7_3": ([5, 5], 0.7, 3), "3_0.1_2": (3, 0.1, 2)}.items():
+        out["lo_" + tag] = denoise_LO(un, sz, lam, it)
+    save("altba.npz", **out)
+
+
 if __name__ == "__main__":
     jobs = sys.argv[1:] or ["unit", "e2e_small", "e2e_synth"]
     for j in jobs:

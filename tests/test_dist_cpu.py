@@ -142,3 +142,23 @@ def test_gather_layout_check_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0] == (True, False)
+
+
+def test_inner_loop_figure():
+    """SURVEY.md §8d inner-loop bytes: N*(48+56+24) per warp + 76*N*K over
+    the warp / assembly / update / CG kernel time."""
+    import bench
+    kt = {"pcg_iter": {"ms_total": 10.0, "launches": 100, "px": 2e8},
+          "pcg_iter.active": {"ms_total": 0.0, "launches": 90, "px": 1.8e8},
+          "partial_deriv_hermite": {"ms_total": 1.0, "launches": 6, "px": 1.2e7},
+          "flow_operator": {"ms_total": 1.0, "launches": 6, "px": 1.2e7},
+          "update_occ": {"ms_total": 0.5, "launches": 6, "px": 1.2e7},
+          "pcg_small": {"ms_total": 0.5, "launches": 6, "px": 1e4},
+          "wmf": {"ms_total": 5.0, "launches": 6, "px": 1.2e7}}
+    pl = {(n, 2000000): r for n, r in kt.items() if n != "pcg_small"}
+    r = bench.inner_loop_of(kt, pl)
+    byt = 1.2e7 * (48 + 56 + 24) + 76 * 1.8e8
+    assert r["bytes_per_step"] == round(byt)
+    assert r["kernel_ms_per_step"] == 13.0  # wmf excluded, pcg_small counted
+    assert r["frac"] == pytest.approx(byt / 13e-3 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert r["finest"]["frac"] == pytest.approx(byt / 12.5e-3 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)

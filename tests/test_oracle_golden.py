@@ -223,3 +223,31 @@ def test_oracle_sor_matches_reference(golden, tag):
     xf = np.concatenate([x[0].ravel(order="F"), x[1].ravel(order="F")])
     assert it == int(s[tag + "_sweeps"])
     assert np.linalg.norm(xf - s[tag + "_x"]) <= 1e-10 * np.linalg.norm(s[tag + "_x"])
+
+
+def test_oracle_altba_nondivergent(golden):
+    """classic-c-a with lambda2 = 0.01 (tests/golden/altba.npz): the oracle
+    within the reference's own chaos (a 1e-12 input perturbation moves the
+    reference by 3.3e-3 px mean, 1.5e-3 median)."""
+    from conftest import epe_stats
+    d = golden("altba.npz")
+    s = epe_stats(O.estimate_flow(d["im1"], d["im2"], "classic-c-a", {"lambda2": 0.01}), d["e2e_lam2_0.01"])
+    assert s["mean"] < 1e-2 and s["median"] < 5e-3, s
+
+
+@pytest.mark.parametrize("alpha,rep", [(1.0, True), (1.0, False), (0.0, True), (0.0, False)])
+def test_oracle_altba_compute_flow_base(golden, alpha, rep):
+    """The oracle's AltBA compute_flow_base(uv, uvhat) vs the reference
+    (tests/golden/altba.npz, gen_golden.py altba): float64 to 1e-8."""
+    from optical_flow.methods.config import load_of_method
+    d = golden("altba.npz")
+    o = load_of_method("classic-c-a")
+    o.images = d["base_images"]
+    o.lambda2 = 0.01
+    o.max_iters = 4
+    o.alpha = alpha
+    o.replacement = rep
+    u, uh = O.alt_ba_flow_base(o, d["base_uv"], d["base_uvhat"])
+    key = f"base_a{int(alpha)}_r{int(rep)}"
+    np.testing.assert_allclose(u, d[key + "_uv"], atol=1e-6)
+    np.testing.assert_allclose(uh, d[key + "_uvhat"], atol=1e-6)
