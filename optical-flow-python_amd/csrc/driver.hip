@@ -680,11 +680,11 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
   const int solver = P->solver;
   if (solver == OF_SOLVER_PCG || solver == OF_SOLVER_BACKSLASH) {
     const bool block = solver == OF_SOLVER_BACKSLASH;
-    float poly[4] = {0.f, 0.f, 0.f, 0.f};
+    float poly[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (block) {
-      double cb[4];
-      cheb_poly(3, CG_CHEB_A, 2.0, cb);
-      for (int i = 0; i < 4; ++i) poly[i] = (float)cb[i];
+      double cb[CG_DEG + 1];
+      cheb_poly(CG_DEG, CG_CHEB_A, 2.0, cb);
+      for (int i = 0; i <= CG_DEG; ++i) poly[i] = (float)cb[i];
     }
     // ring slot of this solve; a slot is reused only after a synchronisation
     // has drained its previous solve
@@ -714,9 +714,9 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
       a.P = b.P;
       a.rtol = block ? P->exact_rtol : P->pcg_rtol;
       a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
-      for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
+      for (int i = 0; i < 8; ++i) a.poly[i] = poly[i];
       a.st = c->d_state;
-      launch(c, "pcg_small", block ? k_cg_small<3, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY), 0,
+      launch(c, "pcg_small", block ? k_cg_small<CG_DEG, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY), 0,
              a);
       HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
       return res;
@@ -757,7 +757,7 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
       ak.part_wr = c->d_partials + (size_t)cur * 5 * PCG_MAX_BLOCKS;
       return ak;
     };
-    for (int i = 0; i < 4; ++i) a.poly[i] = poly[i];
+    for (int i = 0; i < 8; ++i) a.poly[i] = poly[i];
     a.hflag = c->d_flag + slot;
     const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
       const bool odd = W & 1;
@@ -2095,3 +2095,13 @@ int of_median_filter(of_ctx *c, const float *in, int H, int W, int planes, int s
 }
 
 }  // extern "C"
+
+#ifdef CGS_PHASE_TIMING
+// instrumented builds only (tools/micro): read and clear the k_cgs role timers
+extern "C" int of_debug_cgs_times(unsigned long long *out12) {
+  if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_cgs_t), sizeof(unsigned long long) * 12) != hipSuccess) return OF_EHIP;
+  unsigned long long z[12] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_cgs_t), z, sizeof(z)) != hipSuccess) return OF_EHIP;
+  return OF_OK;
+}
+#endif

@@ -13,6 +13,11 @@
 #include "kernels.h"
 
 #define PCG_MAX_BLOCKS 512
+// degree of the Chebyshev polynomial preconditioner of the 'backslash'
+// surrogate (k_cgs, k_cg_small): 5 needs 0.70x the iterations of 3 on
+// Classic+NL stage-2 systems (tools/poly_iters.py), and its two extra stencil
+// stages run on the two waves of a k_cgs block that had idle time
+#define CG_DEG 5
 
 template <bool BLOCK>
 __device__ __forceinline__ float2 precond(float a, float c, float d, float2 r) {
@@ -91,7 +96,7 @@ struct PcgArgs {
   CgFlag *hflag;  // mapped host memory (may be null)
   double rtol;
   int maxiter;
-  float poly[4];  // k_cgs: M^-1 = (poly[0] + poly[1] B + poly[2] B^2 + poly[3] B^3) D^-1
+  float poly[8];  // k_cgs: M^-1 = (poly[0] + poly[1] B + ... + poly[CG_DEG] B^CG_DEG) D^-1
 };
 
 // the shared prologue: returns 1 when the solve is finished (state written)
@@ -541,7 +546,7 @@ struct CgSmallArgs {
   int H, W, P;
   double rtol;
   int maxiter;
-  float poly[4];
+  float poly[8];
   PcgState *st;
 };
 
@@ -629,7 +634,6 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
   const double bnorm = sqrt(rr), atol = g.rtol * bnorm;
   double rho_prev = 1.0;
   int it = 0, done = 0;
-  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
   for (;; ++it) {
     if (rr == 0.0 && it == 0) { done = 3; break; }
     if (sqrt(rr) < atol) { done = 1; break; }
@@ -644,29 +648,41 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
         acc += (double)(rk.x * z.x + rk.y * z.y);
       }
     } else {
+      // Horner: g_DEG-1 = c_DEG-1 y + c_DEG B y, g_i = c_i y + B g_i+1, z = g_0
       CGS_FOR_PIXELS(H, W) {
         const size_t k = (size_t)i * P + j;
         g.y[k] = cgs_minv<BLOCK>(cf, ps, k, g.r[k]);
       }
       __syncthreads();
-      CGS_FOR_PIXELS(H, W) {  // g2 = c2 y + c3 D^-1 N y
+      CGS_FOR_PIXELS(H, W) {
         const size_t k = (size_t)i * P + j;
         const float2 ny = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.y, i, j, H, W, P)), yk = g.y[k];
-        g.t[k] = make_float2(c2 * yk.x + c3 * ny.x, c2 * yk.y + c3 * ny.y);
+        g.t[k] = make_float2(g.poly[DEG - 1] * yk.x + g.poly[DEG] * ny.x, g.poly[DEG - 1] * yk.y + g.poly[DEG] * ny.y);
       }
-      __syncthreads();
-      CGS_FOR_PIXELS(H, W) {  // g1 = c1 y + D^-1 N g2
-        const size_t k = (size_t)i * P + j;
-        const float2 ng = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.t, i, j, H, W, P)), yk = g.y[k];
-        g.q[k] = make_float2(c1 * yk.x + ng.x, c1 * yk.y + ng.y);
+      float2 *src = g.t, *dst = g.q;
+#pragma unroll
+      for (int d = DEG - 2; d >= 0; --d) {
+        __syncthreads();
+        CGS_FOR_PIXELS(H, W) {
+          const size_t k = (size_t)i * P + j;
+          const float2 ng = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, src, i, j, H, W, P)), yk = g.y[k];
+          const float2 v = make_float2(g.poly[d] * yk.x + ng.x, g.poly[d] * yk.y + ng.y);
+          dst[k] = v;
+          if (d == 0) {
+            const float2 rk = g.r[k];
+            acc += (double)(rk.x * v.x + rk.y * v.y);
+          }
+        }
+        float2 *tmp = src;
+        src = dst;
+        dst = tmp;
       }
-      __syncthreads();
-      CGS_FOR_PIXELS(H, W) {  // z = c0 y + D^-1 N g1
-        const size_t k = (size_t)i * P + j;
-        const float2 ng = cgs_minv<BLOCK>(cf, ps, k, cgs_nsum(cf, ps, g.q, i, j, H, W, P)), yk = g.y[k];
-        const float2 z = make_float2(c0 * yk.x + ng.x, c0 * yk.y + ng.y), rk = g.r[k];
-        g.t[k] = z;
-        acc += (double)(rk.x * z.x + rk.y * z.y);
+      if (src != g.t) {  // z into t
+        __syncthreads();
+        CGS_FOR_PIXELS(H, W) {
+          const size_t k = (size_t)i * P + j;
+          g.t[k] = src[k];
+        }
       }
     }
     const double rho = cgs_sum(acc, lds);  // (barrier: t complete)
@@ -708,7 +724,7 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
     g.st->atol = atol;
   }
 }
-template __global__ void k_cg_small<3, true>(CgSmallArgs);
+template __global__ void k_cg_small<CG_DEG, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, false>(CgSmallArgs);
 
@@ -729,7 +745,28 @@ template __global__ void k_cg_small<0, false>(CgSmallArgs);
 // Stage lags follow from one barrier per step: a stage reads rows of another
 // wave produced at earlier steps; the band is walked for n in
 // [r0 - 5, r1 + 8] so that every row a required stage reads was produced.
-#define CGS_NREC 12
+#define CGS_NREC 14
+
+// CGS_PHASE_TIMING (tools/micro builds only): per role, the cycles a wave
+// spends working and waiting at the row-step barriers
+#ifdef CGS_PHASE_TIMING
+__device__ unsigned long long g_cgs_t[4][3];  // [role] {work, wait, waves}
+#define CGS_T0 unsigned long long cgs_wait = 0, cgs_t_start = clock64();
+#define CGS_BAR_BEGIN const unsigned long long cgs_b0 = clock64();
+#define CGS_BAR_END cgs_wait += clock64() - cgs_b0;
+#define CGS_T1                                                           \
+  if (lane == 0) {                                                       \
+    const unsigned long long tot = clock64() - cgs_t_start;              \
+    atomicAdd(&g_cgs_t[wid][0], tot - cgs_wait);                         \
+    atomicAdd(&g_cgs_t[wid][1], cgs_wait);                               \
+    atomicAdd(&g_cgs_t[wid][2], 1ull);                                   \
+  }
+#else
+#define CGS_T0
+#define CGS_BAR_BEGIN
+#define CGS_BAR_END
+#define CGS_T1
+#endif
 
 template <bool FIRST, bool ODD>
 __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands) {
@@ -755,7 +792,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
   const bool live = band < nbands;
   const int r0 = band * R, r1 = min(r0 + R, H);
-  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3];
+  const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3], c4 = g.poly[4], c5 = g.poly[5];
   auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb4 : CG_ROW_OOB); };
   auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb8 : CG_ROW_OOB); };
   auto load_raw = [&](int t, CgRaw &c) {
@@ -818,7 +855,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     return (dm0 ? p.x + p.y : 0.f) + (dm1 ? q.x + q.y : 0.f);
   };
   const cg_f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const int ns = r0 - 5, ne = r1 + 8;
+  const int ns = r0 - 8, ne = r1 + 11;
 
   // zeroed rings: rows above the band that no required stage reads
   {
@@ -831,7 +868,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     }
   }
   // wave 0: raw rows ns-2 .. ns+1, p_old rows ns-2 .. ns+1, r_in row ns-1
-  // wave 2: p_old, x of row ns-6 (register rings indexed by (row - ns))
+  // wave 2: p_old, x of row ns-8 (register rings indexed by (row - ns))
   CgRaw SG[4], SGp[2];
   cg_f4 PO[8], RI[2], PO2[2], XI[2];
   if (live && wid == 0) {
@@ -844,8 +881,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     RI[1] = load_rin(ns - 1);
   }
   if (live && wid == 2) {
-    PO2[0] = load_po(ns - 6);
-    XI[0] = load_x(ns - 6);
+    PO2[0] = load_po(ns - 8);
+    XI[0] = load_x(ns - 8);
   }
   float alpha = 0.f, beta = 0.f;
   if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
@@ -857,6 +894,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       put_rec(ns - 1, SGp[1]);
     }
     __syncthreads();
+    CGS_T0
     // each wave runs its own role's loop (registers of one role only), one
     // block barrier per row step in every role (same step count)
 #define CGS_STEPS(...)                                                    \
@@ -865,9 +903,11 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       const int n = n0 + u;                                               \
       if (n > ne) break;                                                  \
       __VA_ARGS__                                                         \
+      CGS_BAR_BEGIN                                                       \
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");              \
       __builtin_amdgcn_s_barrier();                                       \
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");              \
+      CGS_BAR_END                                                         \
     }                                                                     \
   }
 // register-ring index of row n + d: (u + d) mod ring size
@@ -896,93 +936,128 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         }
       })
     } else if (wid == 1) {
+      // Horner, degree 5: g4 = c4 y + c5 B y (row n-3), g3 = c3 y + B g4
+      // (n-4), g2 = c2 y + B g3 (n-5), g1 = c1 y + B g2 (n-6) -> LDS
+      cg_f4 G4[4] = {zero4, zero4, zero4, zero4}, G3[4] = {zero4, zero4, zero4, zero4};
       cg_f4 G2[4] = {zero4, zero4, zero4, zero4};
+      auto yrow = [&](int t) {
+        const float4 a = s_y[t & 7][lane];
+        return cg_f4{a.x, a.y, a.z, a.w};
+      };
       CGS_STEPS({
-        // B) row n-3: g2 = c2 y + c3 D^-1 N y
         {
-          const CgRec q2 = get_rec(n - 3);
+          const CgRec q = get_rec(n - 3);
           cg_f2 wu[2];
           get_wy(n - 4, wu);
-          const float4 a = s_y[(n - 4) & 7][lane], b = s_y[(n - 3) & 7][lane], c = s_y[(n - 2) & 7][lane];
-          const cg_f4 ym = {a.x, a.y, a.z, a.w}, y0 = {b.x, b.y, b.z, b.w}, yp = {c.x, c.y, c.z, c.w};
-          const cg_f4 ny = cgr_nsum(ym, y0, yp, q2, wu);
-          G2[R4(-3)] = c2 * y0 + c3 * cgr_minv(q2, ny);
+          const cg_f4 y0 = yrow(n - 3);
+          const cg_f4 ny = cgr_nsum(yrow(n - 4), y0, yrow(n - 2), q, wu);
+          G4[R4(-3)] = c4 * y0 + c5 * cgr_minv(q, ny);
         }
-        // C) row n-4: g1 = c1 y + D^-1 N g2
         {
-          const CgRec q3 = get_rec(n - 4);
+          const CgRec q = get_rec(n - 4);
           cg_f2 wu[2];
           get_wy(n - 5, wu);
-          const float4 b = s_y[(n - 4) & 7][lane];
-          const cg_f4 y0 = {b.x, b.y, b.z, b.w};
-          const cg_f4 ng = cgr_nsum(G2[R4(-5)], G2[R4(-4)], G2[R4(-3)], q3, wu);
-          st4(s_g1, n - 4, c1 * y0 + cgr_minv(q3, ng));
+          const cg_f4 ng = cgr_nsum(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
+          G3[R4(-4)] = c3 * yrow(n - 4) + cgr_minv(q, ng);
+        }
+        {
+          const CgRec q = get_rec(n - 5);
+          cg_f2 wu[2];
+          get_wy(n - 6, wu);
+          const cg_f4 ng = cgr_nsum(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
+          G2[R4(-5)] = c2 * yrow(n - 5) + cgr_minv(q, ng);
+        }
+        {
+          const CgRec q = get_rec(n - 6);
+          cg_f2 wu[2];
+          get_wy(n - 7, wu);
+          const cg_f4 ng = cgr_nsum(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, wu);
+          st4(s_g1, n - 6, c1 * yrow(n - 6) + cgr_minv(q, ng));
         }
       })
     } else if (wid == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
       CGS_STEPS({
-        PO2[R2(-5)] = load_po(n - 5);
-        XI[R2(-5)] = load_x(n - 5);
-        // D) row n-6: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
+        PO2[R2(-7)] = load_po(n - 7);
+        XI[R2(-7)] = load_x(n - 7);
+        // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
-          const CgRec q4 = get_rec(n - 6);
+          const CgRec q4 = get_rec(n - 8);
           cg_f2 wu[2];
-          get_wy(n - 7, wu);
-          const cg_f4 ng = cgr_nsum(ld4(s_g1, n - 7), ld4(s_g1, n - 6), ld4(s_g1, n - 5), q4, wu);
-          const float4 b = s_y[(n - 6) & 7][lane];
+          get_wy(n - 9, wu);
+          const cg_f4 ng = cgr_nsum(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
+          const float4 b = s_y[(n - 8) & 7][lane];
           const cg_f4 yr = {b.x, b.y, b.z, b.w};
           const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
-          cg_f4 p = FIRST ? z : z + beta * PO2[R2(-6)];
-          const int o = n - 6;
+          cg_f4 p = FIRST ? z : z + beta * PO2[R2(-8)];
+          const int o = n - 8;
           const bool rv = (unsigned)o < (unsigned)H;
           if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
           if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
-          PP[R4(-6)] = p;
-          ZZ[R2(-6)] = z;
+          PP[R4(-8)] = p;
+          ZZ[R2(-8)] = z;
           if (o >= r0 && o < r1) {
             const unsigned so = soff8 + (unsigned)o * rowb8;
             cg_st4(rpn, so, p);
-            cg_st4(rx, so, FIRST ? zero4 : XI[R2(-6)] + alpha * PO2[R2(-6)]);
+            cg_st4(rx, so, FIRST ? zero4 : XI[R2(-8)] + alpha * PO2[R2(-8)]);
             acc[3] += (double)mdot(yr, ng);
           }
         }
-        // E) row n-7: q = A p, y_q = D^-1 q
+        // E) row n-9: q = A p, y_q = D^-1 q
         {
-          const CgRec q5 = get_rec(n - 7);
+          const CgRec q5 = get_rec(n - 9);
           cg_f2 wu[2];
-          get_wy(n - 8, wu);
-          const cg_f4 pm = PP[R4(-7)];
-          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[R4(-8)], pm, PP[R4(-6)], q5, wu);
+          get_wy(n - 10, wu);
+          const cg_f4 pm = PP[R4(-9)];
+          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
           const cg_f4 yq = cgr_minv(q5, q);
-          st4(s_yq, n - 7, yq);
-          const int o = n - 7;
+          st4(s_yq, n - 9, yq);
+          const int o = n - 9;
           if (o >= r0 && o < r1) {
             acc[0] += (double)mdot(pm, q);
-            acc[1] += (double)mdot(q, ZZ[R2(-7)]);
+            acc[1] += (double)mdot(q, ZZ[R2(-9)]);
             acc[2] += (double)(c0 * mdot(q, yq));
           }
         }
       })
     } else {
-      cg_f4 V1[2] = {zero4, zero4};
+      // q.M^-1 q = sum_i c_i T_i with v0 = y_q, v1 = B v0, v2 = B v1:
+      // T1 = v0.N v0, T2 = v1.N v0 (row n-11); T3 = v1.N v1, T4 = v2.N v1,
+      // T5 = v2.N v2 (row n-12; T5 counts each edge once, by its right /
+      // lower pixel)
+      cg_f4 V1[4] = {zero4, zero4, zero4, zero4}, V2[2] = {zero4, zero4};
       CGS_STEPS({
-        // F) row n-9: N y_q, v1 = D^-1 N y_q, T1..T3
-        const CgRec q6 = get_rec(n - 9);
-        cg_f2 wy7[2];
-        get_wy(n - 10, wy7);
-        const cg_f4 yq = ld4(s_yq, n - 9);
-        const cg_f4 ny = cgr_nsum(ld4(s_yq, n - 10), yq, ld4(s_yq, n - 8), q6, wy7);
-        const cg_f4 v1 = cgr_minv(q6, ny);
-        const cg_f4 vu = V1[R2(-10)];
-        V1[R2(-9)] = v1;
-        const int o = n - 9;
-        if (o >= r0 && o < r1) {
-          const cg_f2 v0 = cg_lo(v1), vv1 = cg_hi(v1);
-          const cg_f2 h0 = cg_left2(q6.wx[1]) * cg_left2(vv1) + wy7[0] * cg_lo(vu);
-          const cg_f2 h1 = q6.wx[0] * v0 + wy7[1] * cg_hi(vu);
-          const cg_f4 t = (c1 * yq + c2 * v1) * ny + (2.0f * c3) * v1 * cg_cat(h0, h1);
-          acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
+        {
+          const CgRec q6 = get_rec(n - 11);
+          cg_f2 wu[2];
+          get_wy(n - 12, wu);
+          const cg_f4 yq = ld4(s_yq, n - 11);
+          const cg_f4 ny = cgr_nsum(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
+          const cg_f4 v1 = cgr_minv(q6, ny);
+          V1[R4(-11)] = v1;
+          const int o = n - 11;
+          if (o >= r0 && o < r1) {
+            const cg_f4 t = (c1 * yq + c2 * v1) * ny;
+            acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
+          }
+        }
+        {
+          const CgRec q7 = get_rec(n - 12);
+          cg_f2 wy7[2];
+          get_wy(n - 13, wy7);
+          const cg_f4 v1 = V1[R4(-12)];
+          const cg_f4 nv = cgr_nsum(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
+          const cg_f4 v2 = cgr_minv(q7, nv);
+          const cg_f4 vu = V2[R2(-13)];
+          V2[R2(-12)] = v2;
+          const int o = n - 12;
+          if (o >= r0 && o < r1) {
+            const cg_f2 w0 = cg_lo(v2), w1 = cg_hi(v2);
+            const cg_f2 h0 = cg_left2(q7.wx[1]) * cg_left2(w1) + wy7[0] * cg_lo(vu);
+            const cg_f2 h1 = q7.wx[0] * w0 + wy7[1] * cg_hi(vu);
+            const cg_f4 t = (c3 * v1 + c4 * v2) * nv + (2.0f * c5) * v2 * cg_cat(h0, h1);
+            acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
+          }
         }
       })
     }
@@ -990,6 +1065,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #undef R4
 #undef R2
 #undef CGS_STEPS
+    CGS_T1
   }
   write_partials<5>(acc, g.part_wr, lds);
 }

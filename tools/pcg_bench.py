@@ -64,9 +64,22 @@ def main():
     call = lambda: ctx.check(lib.of_solve(ctx.handle, C.byref(P), _native.ptr(coef), _native.ptr(rhs), a.h, a.w,  # noqa
                                           _native.ptr(x), C.byref(it), C.byref(rr)))
     call()
+    try:  # instrumented builds (CGS_PHASE_TIMING): per-role k_cgs timers
+        dbg = lib.of_debug_cgs_times
+    except AttributeError:
+        dbg = None
+    buf = (C.c_ulonglong * 12)()
+    if dbg:
+        dbg(buf)
     ctx.check(lib.of_set_profiling(ctx.handle, 1))
     call()
     call()
+    if dbg:
+        dbg(buf)
+        for r in range(4):
+            w, t, n = buf[3 * r], buf[3 * r + 1], max(1, buf[3 * r + 2])
+            print(json.dumps({"role": r, "work_cycles_per_wave": w / n, "barrier_wait_cycles_per_wave": t / n,
+                              "waves": n}), flush=True)
     n = C.c_int(0)
     names = (C.c_char_p * 64)()
     ms = (C.c_double * 64)()
