@@ -519,7 +519,12 @@ __device__ __forceinline__ cg_f4 cgr_diag(const CgRec &m, cg_f4 f) {
   }
   return cg_cat(o[0], o[1]);
 }
-
+// D f from the raw coefficient row (wave 0 still holds it): no inverse
+__device__ __forceinline__ cg_f4 cgr_diag_raw(const CgRaw &c, cg_f4 f) {
+  const cg_f2 u = cg_f2{f.x, f.z}, v = cg_f2{f.y, f.w};
+  const cg_f2 du = c.a * u + c.c * v, dv = c.c * u + c.d * v;
+  return cg_f4{du.x, dv.x, du.y, dv.y};
+}
 
 // ---------------------------------------------------------------------------
 // k_cg_small: a whole CG solve in ONE workgroup, for levels of at most
@@ -876,6 +881,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     load_raw(ns - 1, SGp[1]);
     load_raw(ns, SG[0]);
     load_raw(ns + 1, SG[1]);
+    SG[3] = SGp[1];  // raw row ns-1: stage A's D at the first step
 #pragma unroll
     for (int m = -2; m <= 1; ++m) PO[m & 7] = load_po(ns + m);
     RI[1] = load_rin(ns - 1);
@@ -925,7 +931,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         cg_f2 wu[2];
         get_wy(n - 2, wu);
         cg_f4 r = RI[R2(-1)];
-        if (!FIRST) r -= alpha * (cgr_diag(q1, PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
+        if (!FIRST) r -= alpha * (cgr_diag_raw(SG[R4(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
         const cg_f4 y = cgr_minv(q1, r);
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
