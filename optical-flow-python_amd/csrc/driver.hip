@@ -642,6 +642,10 @@ void cheb_poly(int m, double a, double b, double *cB) {
 // per CU).  Every block writes one slot of the partials buffer, so the grid
 // may not exceed PCG_MAX_BLOCKS blocks: levels wider than PCG_MAX_BLOCKS
 // strips are refused (OF_ENOTSUP), never silently mis-sized.
+// k_cgs blocks per launch: 2 per CU (LDS-bound) on 256 CUs
+#ifndef CGS_TARGET_BLOCKS
+#define CGS_TARGET_BLOCKS PCG_MAX_BLOCKS
+#endif
 int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
   if (H < 1 || W < 1) return OF_EINVAL;
   const int sw = split ? PCG_SWP : PCG_SW;
@@ -649,7 +653,7 @@ int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
   if (nstrips > PCG_MAX_BLOCKS) return OF_ENOTSUP;
   int nbands, R, gy;
   if (split) {
-    nbands = std::max(1, std::min((H + 7) / 8, PCG_MAX_BLOCKS / nstrips));
+    nbands = std::max(1, std::min((H + 7) / 8, CGS_TARGET_BLOCKS / nstrips));
     R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
     gy = nbands;

@@ -31,9 +31,12 @@ __device__ __forceinline__ float bspline3(float t) {
 
 // partial_deriv (derivatives.py:148-296) for one pixel and all channels.
 // (x2, y2) are the 1-based warped coordinates.
+// writes It, Ix, Iy of every channel straight to the output planes (no
+// per-channel register arrays: a runtime-indexed array would live in scratch)
 template <int INTERP>
 __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int P, size_t ps, int i, int j, float x2,
-                                           float y2, float *it, float *ix, float *iy) {
+                                           float y2, float *__restrict__ It, float *__restrict__ Ix,
+                                           float *__restrict__ Iy) {
   const size_t k = (size_t)i * P + j;
   if (INTERP == OF_INTERP_BICUBIC) {
     float fx = floorf(x2), fy = floorf(y2);
@@ -59,17 +62,17 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
         vy += gx * dhy[yi] * z + sx * dhy[yi] * dx + gx * dhy[2 + yi] * dy + sx * dhy[2 + yi] * dxy;
       }
       if (oob) {
-        it[c] = ix[c] = iy[c] = 0.0f;
+        It[o + k] = Ix[o + k] = Iy[o + k] = 0.0f;
       } else {
-        it[c] = v - d.I1[o + k];
-        ix[c] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
-        iy[c] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
+        It[o + k] = v - d.I1[o + k];
+        Ix[o + k] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
+        Iy[o + k] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
       }
     }
   } else {
     const bool out = (x2 > (float)W) || (x2 < 1.0f) || (y2 > (float)H) || (y2 < 1.0f) || !(x2 == x2) || !(y2 == y2);
     if (out) {
-      for (int c = 0; c < d.nc; ++c) it[c] = ix[c] = iy[c] = 0.0f;
+      for (int c = 0; c < d.nc; ++c) It[c * ps + k] = Ix[c * ps + k] = Iy[c * ps + k] = 0.0f;
       return;
     }
     const float r = y2 - 1.0f, q = x2 - 1.0f;
@@ -101,9 +104,9 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
           vx += wr[a] * tx;
           vy += wr[a] * ty;
         }
-        it[c] = v - d.I1[o + k];
-        ix[c] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
-        iy[c] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
+        It[o + k] = v - d.I1[o + k];
+        Ix[o + k] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
+        Iy[o + k] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
       }
     } else {  // bi-linear
       int i0 = (int)floorf(r), j0 = (int)floorf(q);
@@ -115,30 +118,26 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
           const float *r0 = p + o + (size_t)i0 * P, *r1 = p + o + (size_t)i1 * P;
           return (1.0f - fr) * ((1.0f - fc) * r0[j0] + fc * r0[j1]) + fr * ((1.0f - fc) * r1[j0] + fc * r1[j1]);
         };
-        it[c] = bil(d.I2) - d.I1[o + k];
-        ix[c] = d.blend * bil(d.A) + (1.0f - d.blend) * d.I1x[o + k];
-        iy[c] = d.blend * bil(d.B) + (1.0f - d.blend) * d.I1y[o + k];
+        It[o + k] = bil(d.I2) - d.I1[o + k];
+        Ix[o + k] = d.blend * bil(d.A) + (1.0f - d.blend) * d.I1x[o + k];
+        Iy[o + k] = d.blend * bil(d.B) + (1.0f - d.blend) * d.I1y[o + k];
       }
     }
   }
 }
 
-#define OF_MAX_NC 4
 
+// launch bounds = the grid2 block (64 x 4): without them the compiler
+// assumes 1024-thread blocks, caps VGPRs at 128 and spills to scratch
 template <int INTERP>
-__global__ void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H, int W, int P, size_t ps,
-                                float *__restrict__ It, float *__restrict__ Ix, float *__restrict__ Iy) {
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H,
+                                                                int W, int P, size_t ps, float *__restrict__ It,
+                                                                float *__restrict__ Ix, float *__restrict__ Iy) {
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     float2 f = uv[k];
-    float it[OF_MAX_NC], ix[OF_MAX_NC], iy[OF_MAX_NC];
-    warp_pixel<INTERP>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, it, ix, iy);
-    for (int c = 0; c < d.nc; ++c) {
-      It[c * ps + k] = it[c];
-      Ix[c * ps + k] = ix[c];
-      Iy[c * ps + k] = iy[c];
-    }
+    warp_pixel<INTERP>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, It, Ix, Iy);
   }
 }
 template __global__ void k_partial_deriv<0>(DerivArgs, const float2 *, int, int, int, size_t, float *, float *, float *);
@@ -161,7 +160,7 @@ __device__ __forceinline__ float2 ld_uvd(const float2 *uv, const float2 *duv, si
 }
 
 // coef planes: 0 wx_u, 1 wy_u, 2 wx_v, 3 wy_v, 4 a_uu, 5 a_uv, 6 a_vv; rhs float2
-__global__ void k_flow_operator(OpArgs o, const float2 *__restrict__ uv, const float2 *__restrict__ duv,
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const float2 *__restrict__ uv, const float2 *__restrict__ duv,
                                 const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
                                 int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
@@ -308,7 +307,7 @@ __device__ __forceinline__ float median_window(const float *a) {
 }
 
 template <int S>
-__global__ void k_median2(const float2 *__restrict__ in, float2 *__restrict__ out, int H, int W, int P) {
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_median2(const float2 *__restrict__ in, float2 *__restrict__ out, int H, int W, int P) {
   constexpr int h = S / 2;
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
@@ -329,7 +328,7 @@ __global__ void k_median2(const float2 *__restrict__ in, float2 *__restrict__ ou
 }
 
 template <int S>
-__global__ void k_median1(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps) {
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_median1(const float *__restrict__ in, float *__restrict__ out, int H, int W, int P, size_t ps) {
   constexpr int h = S / 2;
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
@@ -386,6 +385,7 @@ __global__ void k_lo_blend(const float2 *__restrict__ u, const float2 *__restric
 // (weighted_median.py:5-21, :67-112): the cumulative sum at a sorted sample
 // is (chunk prefix) + (in-window weights before it in the chunk), the same
 // sums the reference forms, summed in another order.
+#define OF_MAX_NC 4  // image channels per frame the host accepts
 #define WMF_T 8
 #ifdef WMF_PHASE_TIMING  // tools/micro/wmf_phases.hip: per-wave phase timestamps
 extern __device__ unsigned long long g_wmf_t[];
