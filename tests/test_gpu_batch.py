@@ -112,13 +112,15 @@ def test_rccl_gather_single_rank():
         ctx.close()
 
 
-@pytest.mark.parametrize("lanes,n,H,W", [(1, 3, 60, 88), (2, 5, 60, 88), (3, 4, 270, 480)])
+@pytest.mark.parametrize("lanes,n,H,W", [(1, 3, 60, 88), (2, 5, 60, 88), (3, 4, 270, 480), (3, 3, 540, 960)])
 def test_pairs_run_host_matches_estimate_flow(lanes, n, H, W):
     """of_pairs_run_host (uint8 frames in host memory -> flows in host
     memory, uploads/downloads overlapped on copy streams) equals
     estimate_flow on every pair bitwise (same kernels; the bytes path
     computes gray/Lab from the same integer values), for any lane count;
-    the flows also stay in device slots 0..n-1."""
+    the flows also stay in device slots 0..n-1.  At 540x960 three lanes run
+    3 x 504 k_cgs blocks at once, more than the 512 that are resident: the
+    ping-ponged CG partials must keep every lane's result exact."""
     import optical_flow
     from optical_flow import _native
     from optical_flow.utils.synthetic import synth_pair
