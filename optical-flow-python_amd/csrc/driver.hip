@@ -320,8 +320,15 @@ Taps make_taps(const double *k, int kh, int kw) {
 }
 void correlate(of_ctx *c, const Img &in, const Img &out, const Taps &t) {
   Grid2 g = grid2(in.H, in.W);
-  launch(c, "correlate", k_correlate, gz(g, in.C), g.block, 0, (const float *)in.p, out.p, in.H, in.W, in.P, in.ps(),
-         t);
+  const bool fold1 = in.H > t.kh / 2 && in.W > t.kw / 2;  // one reflection reaches every tap
+  auto go = [&](auto k) {
+    launch(c, "correlate", k, gz(g, in.C), g.block, 0, (const float *)in.p, out.p, in.H, in.W, in.P, in.ps(), t);
+  };
+  if (fold1 && t.kh == 5 && t.kw == 5) go(k_correlate_k<5, 5>);
+  else if (fold1 && t.kh == 1 && t.kw == 5) go(k_correlate_k<1, 5>);
+  else if (fold1 && t.kh == 5 && t.kw == 1) go(k_correlate_k<5, 1>);
+  else if (fold1 && t.kh == 3 && t.kw == 3) go(k_correlate_k<3, 3>);
+  else go(k_correlate);
 }
 
 // fspecial('gaussian') (image_processing.py:29-49)
@@ -935,6 +942,38 @@ struct LevelIn {
   Img guide;  // gc planes or p == nullptr
 };
 
+// Lanes mode (of_pairs_run): a phase on a level of >= big_px pixels (the
+// full-size preprocessing and every fine CG solve) holds the lanes' shared
+// token until its GPU work has drained, so at most one pair at a time streams
+// a fine CG working set (1080p: ~190 MB, most of the 256 MB Infinity Cache)
+// and two lanes' 512-block CG launches never interleave.  Outside lanes
+// mode: no-op.
+struct BigPhase {
+  of_ctx *c;
+  bool held = false;
+  BigPhase(of_ctx *c_, double px) : c(c_) {
+    if (c->big && px >= c->big_px) {
+      c->big->lock();
+      held = true;
+    }
+  }
+  ~BigPhase() {
+    if (held) {
+      hipStreamSynchronize(c->stream);
+      c->big->unlock();
+    }
+  }
+};
+
+// Only the fine solves hold the token: a fine level's assembly, warps and
+// weighted median (VALU/LDS-bound) overlap another lane's CG (issue- and
+// HBM-bound); measured 33.8 -> 34.5 pairs/s at 3 lanes vs holding the token
+// through whole fine levels
+SolveResult solve_tok(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+  BigPhase bp(c, (double)b.H * b.W);
+  return solve(c, P, coef, b, x);
+}
+
 // HSOpticalFlow.compute_flow_base (hs.py:109-142)
 void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
@@ -948,7 +987,7 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
   for (int it = 0; it < P->max_warping_iters; ++it) {
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
-    note_solve(c, st, solve(c, P, coef, rhs, x));
+    note_solve(c, st, solve_tok(c, P, coef, rhs, x));
     c->cur_px = (double)H * W;
     if (std::sqrt(norm2(c, x)) < 1e-3) break;
     launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)x.p, P->limit_update, H, W, uv.P);
@@ -980,7 +1019,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     for (int jl = 0; jl < max_linear; ++jl) {
       flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
-      note_solve(c, st, solve(c, P, coef, rhs, x));
+      note_solve(c, st, solve_tok(c, P, coef, rhs, x));
       c->cur_px = (double)H * W;
       const bool filt = P->median_filter_size != 0;
       launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
@@ -1024,7 +1063,7 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
     bool have_duv = false;
     for (int jl = 0; jl < P->max_linear; ++jl) {
       flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
-      note_solve(c, st, solve(c, P, coef, rhs, x));
+      note_solve(c, st, solve_tok(c, P, coef, rhs, x));
       c->cur_px = (double)H * W;
       // duv = clip(x): computed as (0 + clip(x))
       HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
@@ -1066,28 +1105,6 @@ void check_params(const of_params *P) {
               P->median_filter_size == 7,
           OF_ENOTSUP, "median_filter_size must be None, 3, 5 or 7");
 }
-
-// Lanes mode (of_pairs_run): a phase whose level has >= big_px pixels holds
-// the lanes' shared token until its GPU work has drained, so at most one pair
-// at a time streams a fine level's working set (1080p CG: ~190 MB, most of
-// the 256 MB Infinity Cache) while the other lanes run coarse levels, which
-// are latency-bound and need few bytes.  Outside lanes mode: no-op.
-struct BigPhase {
-  of_ctx *c;
-  bool held = false;
-  BigPhase(of_ctx *c_, double px) : c(c_) {
-    if (c->big && px >= c->big_px) {
-      c->big->lock();
-      held = true;
-    }
-  }
-  ~BigPhase() {
-    if (held) {
-      hipStreamSynchronize(c->stream);
-      c->big->unlock();
-    }
-  }
-};
 
 // compute_flow (hs.py:49-99, ba.py:57-138, classic_nl.py:89-198, alt_ba.py:81-187)
 // images: device 2nc planes; guide: device gc planes or p == nullptr;
@@ -1148,7 +1165,6 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
     for (int l = nl - 1; l >= 0; --l) {
       const int h = lv[l].H, w = lv[l].W;
       hipEvent_t e0 = timing_event(c), e1 = timing_event(c);
-      BigPhase bp(c, (double)h * w);
       HIPCHK(hipEventRecord(e0, c->stream));
       if (uv.H != h || uv.W != w) {
         F2 nuv = new_f2(c, h, w);

@@ -239,6 +239,35 @@ __global__ void k_correlate(const float *__restrict__ in, float *__restrict__ ou
   }
 }
 
+// the same with the kernel size fixed at compile time (taps unrolled into
+// registers) and one-fold reflection, valid while the radius is below the
+// plane size (host-checked): no integer modulo per tap
+__device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i - 1 : (i >= n ? 2 * n - 1 - i : i); }
+template <int KH, int KW>
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_correlate_k(const float *__restrict__ in, float *__restrict__ out,
+                                                             int H, int W, int P, size_t ps, Taps t) {
+  in += blockIdx.z * ps;
+  out += blockIdx.z * ps;
+  constexpr int ch = KH / 2, cw = KW / 2;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    int cols[KW];
+#pragma unroll
+    for (int b = 0; b < KW; ++b) cols[b] = refl1(j + b - cw, W);
+    float s = 0.0f;
+#pragma unroll
+    for (int a = 0; a < KH; ++a) {
+      const float *row = in + (size_t)refl1(i + a - ch, H) * P;
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        const float w = t.w[a * KW + b];
+        if (w != 0.0f) s += w * row[cols[b]];
+      }
+    }
+    out[(size_t)i * P + j] = s;
+  }
+}
+
 // _matlab_imresize_bilinear / resample_flow: source coordinate
 // (o + 0.5) * (H / nH) - 0.5 clipped to [0, H-1], bilinear, times `mult`.
 template <typename T>
