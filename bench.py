@@ -19,8 +19,10 @@ of_pairs_run) is reported beside it as `device_resident`.
 Also reported (one JSON line on rank 0):
   roofline      dominant HBM kernel: algorithmic bytes per launch / mean
                 HIP-event duration of that kernel over a profiled replay of
-                one timed step (same pairs and lanes); peak 8 TB/s; traffic
-                from profiles/ PMC if present (else null)
+                the step's pairs one at a time (lanes = 1; the lanes replay
+                beside it as `concurrent`); inner_loop = SURVEY.md §8d's
+                "SOR/PCG + warp" figure; peak 8 TB/s; traffic from profiles/
+                PMC if present (else null)
   cpu_baseline  the float64 C oracle (oracle/, OpenMP) on a bounded crop of
                 the same pair, scaled by pixel count to pairs/s
   ms_per_level  GPU time of each compute_flow_base (coarse -> fine, per stage)
@@ -370,16 +372,23 @@ def main():
         # profiled replay of one step, same pairs and lanes as the timed
         # steps: HIP events around every launch on the stream it runs on
         ktimes, per_level = profiled_replay(ctx, lib, P0, args.pairs, args.lanes)
-        roofline = roofline_of(ktimes, per_level)
         pcg_levels = [{"px": px, "ms": round(rec["ms_total"] / args.pairs, 3), "launches": rec["launches"] / args.pairs,
                        "active": per_level.get(("pcg_iter.active", px), {}).get("launches", 0) / args.pairs}
                       for (n, px), rec in sorted(per_level.items(), key=lambda kv: -kv[0][1]) if n == "pcg_iter"]
-        inner = inner_loop_of(ktimes, per_level)
-        # the same pairs one at a time (lanes = 1): kernel durations without a
-        # second pipeline's kernels sharing the CUs
+        # the roofline proper: the same pairs one at a time (lanes = 1), so a
+        # kernel's duration is its own, not stretched by another lane's
+        # kernels sharing the CUs (profiles/: rocprofv3 of bench.py --lanes 1)
         kt1, pl1 = profiled_replay(ctx, lib, P0, args.pairs, 1)
-        inner["isolated"] = inner_loop_of(kt1, pl1)
+        roofline = roofline_of(kt1, pl1)
         if roofline is not None:
+            roofline["replay"] = "isolated: lanes=1 over the step's pairs"
+            inner = inner_loop_of(kt1, pl1)
+            rc = roofline_of(ktimes, per_level)
+            conc = inner_loop_of(ktimes, per_level)
+            roofline["concurrent"] = {
+                "replay": f"lanes={args.lanes} as timed; durations include co-running kernels of other lanes",
+                "achieved": rc["achieved"], "frac": rc["frac"], "mean_launch_ms": rc["mean_launch_ms"],
+                "inner_loop_frac": conc["frac"] if conc else None}
             roofline["inner_loop"] = inner
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
