@@ -3,7 +3,8 @@
 Host-side API utilities with the semantics of the reference's
 optical_flow/robust/penalties.py:18-373 (d_type 0 = value, 1 = derivative,
 2 = derivative / x, the IRLS weight).  The GPU hot path does not call these:
-it evaluates the same formulas in-kernel (csrc/penalty.h).
+it evaluates the same weights in-kernel (csrc/common.h: pen_w), checked
+against the oracle for every kind in tests/test_gpu_reference_cases.py.
 """
 import numpy as np
 from scipy.special import gammaln
