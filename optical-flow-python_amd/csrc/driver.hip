@@ -328,6 +328,8 @@ void correlate(of_ctx *c, const Img &in, const Img &out, const Taps &t) {
   else if (fold1 && t.kh == 1 && t.kw == 5) go(k_correlate_k<1, 5>);
   else if (fold1 && t.kh == 5 && t.kw == 1) go(k_correlate_k<5, 1>);
   else if (fold1 && t.kh == 3 && t.kw == 3) go(k_correlate_k<3, 3>);
+  else if (fold1 && t.kh == 1 && t.kw == 3) go(k_correlate_k<1, 3>);
+  else if (fold1 && t.kh == 3 && t.kw == 1) go(k_correlate_k<3, 1>);
   else go(k_correlate);
 }
 
@@ -357,6 +359,26 @@ void resize_dims(int H, int W, double ratio, int *nH, int *nW) {
 }
 
 // one compute_image_pyramid step (pyramid.py:58-67)
+// a separable kh x kw kernel ky (x) kx as a row pass then a column pass
+// (10 taps per pixel instead of 25 for 5 x 5; same sums, another rounding order)
+void correlate_sep(of_ctx *c, const Img &in, const Img &out, const Taps &tx, const Taps &ty) {
+  Img tmp = new_img(c, in.H, in.W, in.C);
+  correlate(c, in, tmp, tx);
+  correlate(c, tmp, out, ty);
+}
+
+Img pyramid_step(of_ctx *c, const Img &in, const Taps &tx, const Taps &ty, double ratio) {
+  int nH, nW;
+  resize_dims(in.H, in.W, ratio, &nH, &nW);
+  Img tmp = new_img(c, in.H, in.W, in.C);
+  correlate_sep(c, in, tmp, tx, ty);
+  Img out = new_img(c, nH, nW, in.C);
+  Grid2 g = grid2(nH, nW);
+  launch(c, "resize", k_resize<float>, gz(g, in.C), g.block, 0, (const float *)tmp.p, in.H, in.W, in.P, tmp.ps(),
+         out.p, nH, nW, out.P, out.ps(), 1.0f);
+  return out;
+}
+
 Img pyramid_step(of_ctx *c, const Img &in, const Taps &t, double ratio) {
   int nH, nW;
   resize_dims(in.H, in.W, ratio, &nH, &nW);
@@ -373,10 +395,16 @@ Img pyramid_step(of_ctx *c, const Img &in, const Taps &t, double ratio) {
 std::vector<Img> build_pyramid(of_ctx *c, const Img &img, int levels, double spacing) {
   double sig = std::sqrt(spacing) / std::sqrt(2.0);
   int ks = 2 * (int)std::nearbyint(1.5 * sig) + 1;
-  auto k = gaussian(ks, sig);
-  Taps t = make_taps(k.data(), ks, ks);
+  // fspecial('gaussian') is the outer product of the normalised 1-D
+  // Gaussian (its eps cut-off removes nothing at these sizes: the smallest
+  // entry is >= 1.8 % of the largest)
+  std::vector<double> g1(ks);
+  double s1 = 0.0;
+  for (int b = 0; b < ks; ++b) s1 += (g1[b] = std::exp(-(b - (ks - 1) / 2.0) * (b - (ks - 1) / 2.0) / (2 * sig * sig)));
+  for (auto &v : g1) v /= s1;
+  const Taps tx = make_taps(g1.data(), 1, ks), ty = make_taps(g1.data(), ks, 1);
   std::vector<Img> pyr{img};
-  for (int l = 1; l < levels; ++l) pyr.push_back(pyramid_step(c, pyr.back(), t, 1.0 / spacing));
+  for (int l = 1; l < levels; ++l) pyr.push_back(pyramid_step(c, pyr.back(), tx, ty, 1.0 / spacing));
   return pyr;
 }
 
@@ -425,10 +453,9 @@ LevelDeriv level_deriv(of_ctx *c, const Img &im, int nc, int interp, const doubl
   correlate(c, I2, L.A, tx);
   correlate(c, I2, L.B, ty);
   if (interp == OF_INTERP_BICUBIC) {
-    double kxy[25];
-    for (int a = 0; a < 5; ++a)
-      for (int b = 0; b < 5; ++b) kxy[a * 5 + b] = filt[a] * filt[b];
-    correlate(c, I2, L.Cc, make_taps(kxy, 5, 5));
+    // DXY = correlate(I2, filt^T filt) (derivatives.py:27-145), separably:
+    // the row pass is A itself
+    correlate(c, L.A, L.Cc, ty);
   } else if (interp == OF_INTERP_CUBIC) {
     // B-spline coefficients of I2x, I2y (in place via tmp) and of I2 (into Cc)
     BsplTaps bt;

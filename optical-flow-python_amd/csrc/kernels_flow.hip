@@ -494,10 +494,18 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
 template <int GC, int NPER, int HS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
                                              const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
-                                             int P, size_t ps, int hsz_rt, float nk, int RW, int RP) {
+                                             int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt) {
   using T = typename WmfRec<GC>::T;
   constexpr int N = NPER * 64, CH = N / WMF_NC;
   const int hsz = HS > 0 ? HS : hsz_rt;
+  // region width and record pitch: compile-time with HS (no runtime divides)
+  constexpr int RWc = WMF_T + 2 * HS, RPc = RWc + ((8 - RWc) % 16 + 16) % 16;
+  const int RW = HS > 0 ? RWc : RW_rt, RP = HS > 0 ? RPc : RP_rt;
+  // whole-sample reflect with one fold reaches every region sample when the
+  // plane has >= WMF_T + hsz rows / columns (all pyramid levels of the
+  // registry); otherwise the general modulo form
+  const bool fold1 = H >= WMF_T + hsz && W >= WMF_T + hsz;
+  auto mir = [&](int i, int n) { return fold1 ? (i < 0 ? -i : (i >= n ? 2 * (n - 1) - i : i)) : ext_mirror(i, n); };
   const int nreg = RW * RW;
   // LDS: chunk sums [2][WMF_NC][64] f64 (u chunks, then v chunks; a chunk's
   // 64 lane slots are contiguous, so a scatter-add never conflicts) | records
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     b[r] = ~0ull;
     if (s < nreg) {
       const int ry = s / RW, rx = s - ry * RW;
-      const size_t g = (size_t)ext_mirror(ty0 - hsz + ry, H) * P + ext_mirror(tx0 - hsz + rx, W);
+      const size_t g = (size_t)mir(ty0 - hsz + ry, H) * P + mir(tx0 - hsz + rx, W);
       const float2 v = uv[g];
       const uint64_t lo = ((uint64_t)ry << 8) | (uint64_t)rx;
       a[r] = ((uint64_t)f2ord(v.x) << 32) | lo;
@@ -651,8 +659,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   WMF_STAMP(5);
   if (gi < H && gj < W) {
     // the selected samples' values, re-read at their (mirrored) positions
-    const int ya = ext_mirror(ty0 - hsz + (int)(resu >> 8), H), xa = ext_mirror(tx0 - hsz + (int)(resu & 0xffu), W);
-    const int yb = ext_mirror(ty0 - hsz + (int)(resv >> 8), H), xb = ext_mirror(tx0 - hsz + (int)(resv & 0xffu), W);
+    const int ya = mir(ty0 - hsz + (int)(resu >> 8), H), xa = mir(tx0 - hsz + (int)(resu & 0xffu), W);
+    const int yb = mir(ty0 - hsz + (int)(resv >> 8), H), xb = mir(tx0 - hsz + (int)(resv & 0xffu), W);
     out[(size_t)gi * P + gj] = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
   }
 }
