@@ -111,7 +111,7 @@ __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds
     const double atol = k == 1 ? g.rtol * rn : g.st->atol;
     int done = 0;
     if (k == 1 && S[4] == 0.0) done = 3;
-    else if (rn < atol) done = 1;
+    else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
     else if (k - 1 >= g.maxiter) done = 2;
     const double al = S[3] / S[0];
     const double rho = S[3] - 2.0 * al * S[1] + al * al * S[2];
@@ -290,7 +290,7 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       const double rn = sqrt(S[4]);
       const double atol = k == 1 ? g.rtol * rn : st_atol;
       if (k == 1 && S[4] == 0.0) done = 3;
-      else if (rn < atol) done = 1;
+      else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
       else if (k - 1 >= g.maxiter) done = 2;
       const double a_ = S[3] / S[0];
       const double rho = S[3] - 2.0 * a_ * S[1] + a_ * a_ * S[2];
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
   int it = 0, done = 0;
   for (;; ++it) {
     if (rr == 0.0 && it == 0) { done = 3; break; }
-    if (sqrt(rr) < atol) { done = 1; break; }
+    if (sqrt(rr) < atol || rr == 0.0) { done = 1; break; }
     if (it >= g.maxiter) { done = 2; break; }
     // z = M^-1 r (into t), rho = r.z
     acc = 0.0;
@@ -788,24 +788,42 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
   const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
   const unsigned ps4 = (unsigned)(g.ps * 4);
-  const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = blockIdx.y;
+  // XCD-aware tile order: blocks b, b + 8, b + 16 ... share an XCD's L2
+  // (MI355X_MICROARCH.md, workgroup dispatch), so give each XCD a contiguous
+  // run of row-major tiles; its neighbours' column halos are then read
+  // through the same L2 at about the same row step
+  const int nt = gridDim.x * gridDim.y, lin = blockIdx.x + blockIdx.y * gridDim.x;
+  const int xcd = lin & 7, tile = xcd * (nt >> 3) + min(xcd, nt & 7) + (lin >> 3);
+  const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = tile / gridDim.x;
   const int tid = lane + wid * 64;
-  const int jc = blockIdx.x * PCG_SWP - 8 + 2 * lane;
+  const int jc = (tile - band * gridDim.x) * PCG_SWP - 8 + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
   const bool out_lane = lane >= 4 && lane <= 59;
   const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
   const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
   const bool live = band < nbands;
-  const int r0 = band * R, r1 = min(r0 + R, H);
+  // odd bands walk bottom to top, so each band meets its neighbours' halo
+  // rows at the same row step (both at the start or both at the end of the
+  // walk) and the second read of those rows is served by the XCD's L2.  The
+  // walk runs in virtual rows t (orig row H-1-t when flipped); the lower
+  // edge of virtual row t is the upper edge of its orig row, i.e. the wy
+  // stored at orig row H-2-t.
+  const bool flip = band & 1;
+  const int rb0 = band * R, rb1 = min(rb0 + R, H);
+  const int r0 = flip ? H - rb1 : rb0, r1 = flip ? H - rb0 : rb1;
   const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3], c4 = g.poly[4], c5 = g.poly[5];
-  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb4 : CG_ROW_OOB); };
-  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? (unsigned)t * rowb8 : CG_ROW_OOB); };
+  auto orow = [&](int t) { return (unsigned)(flip ? H - 1 - t : t); };
+  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? orow(t) * rowb4 : CG_ROW_OOB); };
+  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? orow(t) * rowb8 : CG_ROW_OOB); };
+  auto o4w = [&](int t) {
+    return flip ? off4 + ((unsigned)t < (unsigned)(H - 1) ? (unsigned)(H - 2 - t) * rowb4 : CG_ROW_OOB) : o4(t);
+  };
   auto load_raw = [&](int t, CgRaw &c) {
-    const unsigned v = o4(t);
+    const unsigned v = o4(t), vw = o4w(t);
     c.wxu = cg_mask1<ODD>(cg_ld2(rc, v, 0), ok1);
-    c.wyu = cg_mask1<ODD>(cg_ld2(rc, v, ps4), ok1);
+    c.wyu = cg_mask1<ODD>(cg_ld2(rc, vw, ps4), ok1);
     c.wxv = cg_mask1<ODD>(cg_ld2(rc, v, 2 * ps4), ok1);
-    c.wyv = cg_mask1<ODD>(cg_ld2(rc, v, 3 * ps4), ok1);
+    c.wyv = cg_mask1<ODD>(cg_ld2(rc, vw, 3 * ps4), ok1);
     c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
     c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
     c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
@@ -936,7 +954,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
         if (o >= r0 && o < r1) {
-          cg_st4(rro, soff8 + (unsigned)o * rowb8, r);
+          cg_st4(rro, soff8 + orow(o) * rowb8, r);
           acc[4] += (double)mdot(r, r);
           acc[3] += (double)(c0 * mdot(r, y));
         }
@@ -1003,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           PP[R4(-8)] = p;
           ZZ[R2(-8)] = z;
           if (o >= r0 && o < r1) {
-            const unsigned so = soff8 + (unsigned)o * rowb8;
+            const unsigned so = soff8 + orow(o) * rowb8;
             cg_st4(rpn, so, p);
             cg_st4(rx, so, FIRST ? zero4 : XI[R2(-8)] + alpha * PO2[R2(-8)]);
             acc[3] += (double)mdot(yr, ng);
