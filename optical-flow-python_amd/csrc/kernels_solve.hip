@@ -112,6 +112,7 @@ __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds
     int done = 0;
     if (k == 1 && S[4] == 0.0) done = 3;
     else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
+    else if (!(S[0] > 0.0) || !(S[3] > 0.0)) done = 1;  // fp32 underflow (cg_prologue)
     else if (k - 1 >= g.maxiter) done = 2;
     const double al = S[3] / S[0];
     const double rho = S[3] - 2.0 * al * S[1] + al * al * S[2];
@@ -291,6 +292,10 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       const double atol = k == 1 ? g.rtol * rn : st_atol;
       if (k == 1 && S[4] == 0.0) done = 3;
       else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
+      // p.Ap or r.z underflowed in fp32 (rtol 0 runs past the representable
+      // residual; A and M are SPD, so only rounding makes them vanish):
+      // nothing left to divide either
+      else if (!(S[0] > 0.0) || !(S[3] > 0.0)) done = 1;
       else if (k - 1 >= g.maxiter) done = 2;
       const double a_ = S[3] / S[0];
       const double rho = S[3] - 2.0 * a_ * S[1] + a_ * a_ * S[2];
@@ -708,6 +713,7 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
       acc += (double)(pk.x * qk.x + pk.y * qk.y);
     }
     const double pq = cgs_sum(acc, lds);
+    if (!(pq > 0.0) || !(rho > 0.0)) { done = 1; break; }  // underflow (see cg_prologue)
     const float alpha = (float)(rho / pq);
     acc = 0.0;
     CGS_FOR_PIXELS(H, W) {
@@ -751,6 +757,21 @@ template __global__ void k_cg_small<0, false>(CgSmallArgs);
 // wave produced at earlier steps; the band is walked for n in
 // [r0 - 5, r1 + 8] so that every row a required stage reads was produced.
 #define CGS_NREC 14
+// Load distance in row steps (each step ends at a block barrier, so a load
+// issued at step n is waited for at step n + distance): wave 0's coefficient,
+// p_old and r_in rows (CGS_PF), wave 2's p_old and x rows (CGS_PF2).  Ring
+// sizes are powers of two dividing the 8-step unroll.
+#ifndef CGS_PF
+#define CGS_PF 2
+#endif
+#ifndef CGS_PF2
+#define CGS_PF2 1
+#endif
+#define CGS_POW2(n) ((n) <= 1 ? 1 : (n) <= 2 ? 2 : (n) <= 4 ? 4 : 8)
+#define CGS_SGN CGS_POW2(CGS_PF + 2)
+#define CGS_RIN CGS_POW2(CGS_PF + 1)
+#define CGS_W2N CGS_POW2(CGS_PF2 + 1)
+static_assert(CGS_PF >= 1 && CGS_PF + 3 <= 8 && CGS_PF2 >= 1 && CGS_PF2 + 1 <= 8, "k_cgs load distances");
 
 // CGS_PHASE_TIMING (tools/micro builds only): per role, the cycles a wave
 // spends working and waiting at the row-step barriers
@@ -890,23 +911,28 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       (&s_yq[0][0])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // wave 0: raw rows ns-2 .. ns+1, p_old rows ns-2 .. ns+1, r_in row ns-1
-  // wave 2: p_old, x of row ns-8 (register rings indexed by (row - ns))
-  CgRaw SG[4], SGp[2];
-  cg_f4 PO[8], RI[2], PO2[2], XI[2];
+  // wave 0: raw rows ns-2 .. ns+PF-1, p_old rows ns-2 .. ns+PF-1, r_in rows
+  // ns-1 .. ns+PF-2; wave 2: p_old, x of rows ns-8 .. ns-9+PF2 (register
+  // rings indexed by (row - ns) mod ring size)
+  CgRaw SG[CGS_SGN], SGp[2];
+  cg_f4 PO[8], RI[CGS_RIN], PO2[CGS_W2N], XI[CGS_W2N];
   if (live && wid == 0) {
     load_raw(ns - 2, SGp[0]);
     load_raw(ns - 1, SGp[1]);
-    load_raw(ns, SG[0]);
-    load_raw(ns + 1, SG[1]);
-    SG[3] = SGp[1];  // raw row ns-1: stage A's D at the first step
 #pragma unroll
-    for (int m = -2; m <= 1; ++m) PO[m & 7] = load_po(ns + m);
-    RI[1] = load_rin(ns - 1);
+    for (int m = 0; m < CGS_PF; ++m) load_raw(ns + m, SG[m]);
+    SG[CGS_SGN - 1] = SGp[1];  // raw row ns-1: stage A's D at the first step
+#pragma unroll
+    for (int m = -2; m < CGS_PF; ++m) PO[m & 7] = load_po(ns + m);
+#pragma unroll
+    for (int m = -1; m < CGS_PF - 1; ++m) RI[(m + 16) & (CGS_RIN - 1)] = load_rin(ns + m);
   }
   if (live && wid == 2) {
-    PO2[0] = load_po(ns - 8);
-    XI[0] = load_x(ns - 8);
+#pragma unroll
+    for (int m = -8; m < CGS_PF2 - 8; ++m) {
+      PO2[(m + 16) & (CGS_W2N - 1)] = load_po(ns + m);
+      XI[(m + 16) & (CGS_W2N - 1)] = load_x(ns + m);
+    }
   }
   float alpha = 0.f, beta = 0.f;
   if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
@@ -938,18 +964,21 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #define R8(d) ((u + (d) + 16) & 7)
 #define R4(d) ((u + (d) + 16) & 3)
 #define R2(d) ((u + (d) + 16) & 1)
+#define RSG(d) ((u + (d) + 16) & (CGS_SGN - 1))
+#define RRI(d) ((u + (d) + 16) & (CGS_RIN - 1))
+#define RW2(d) ((u + (d) + 16) & (CGS_W2N - 1))
     if (wid == 0) {
       CGS_STEPS({
-        load_raw(n + 2, SG[R4(2)]);
-        PO[R8(2)] = load_po(n + 2);
-        RI[R2(0)] = load_rin(n);
-        put_rec(n, SG[R4(0)]);
+        load_raw(n + CGS_PF, SG[RSG(CGS_PF)]);
+        PO[R8(CGS_PF)] = load_po(n + CGS_PF);
+        RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
+        put_rec(n, SG[RSG(0)]);
         // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
         const CgRec q1 = get_rec(n - 1);
         cg_f2 wu[2];
         get_wy(n - 2, wu);
-        cg_f4 r = RI[R2(-1)];
-        if (!FIRST) r -= alpha * (cgr_diag_raw(SG[R4(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
+        cg_f4 r = RI[RRI(-1)];
+        if (!FIRST) r -= alpha * (cgr_diag_raw(SG[RSG(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
         const cg_f4 y = cgr_minv(q1, r);
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
@@ -1002,8 +1031,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     } else if (wid == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
       CGS_STEPS({
-        PO2[R2(-7)] = load_po(n - 7);
-        XI[R2(-7)] = load_x(n - 7);
+        PO2[RW2(CGS_PF2 - 8)] = load_po(n + CGS_PF2 - 8);
+        XI[RW2(CGS_PF2 - 8)] = load_x(n + CGS_PF2 - 8);
         // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
           const CgRec q4 = get_rec(n - 8);
@@ -1013,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           const float4 b = s_y[(n - 8) & 7][lane];
           const cg_f4 yr = {b.x, b.y, b.z, b.w};
           const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
-          cg_f4 p = FIRST ? z : z + beta * PO2[R2(-8)];
+          cg_f4 p = FIRST ? z : z + beta * PO2[RW2(-8)];
           const int o = n - 8;
           const bool rv = (unsigned)o < (unsigned)H;
           if (!(rv && ok0)) { p.x = 0.f; p.y = 0.f; }
@@ -1023,7 +1052,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           if (o >= r0 && o < r1) {
             const unsigned so = soff8 + orow(o) * rowb8;
             cg_st4(rpn, so, p);
-            cg_st4(rx, so, FIRST ? zero4 : XI[R2(-8)] + alpha * PO2[R2(-8)]);
+            cg_st4(rx, so, FIRST ? zero4 : XI[RW2(-8)] + alpha * PO2[RW2(-8)]);
             acc[3] += (double)mdot(yr, ng);
           }
         }
@@ -1088,6 +1117,9 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #undef R8
 #undef R4
 #undef R2
+#undef RSG
+#undef RRI
+#undef RW2
 #undef CGS_STEPS
     CGS_T1
   }
