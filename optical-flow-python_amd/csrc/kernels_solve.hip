@@ -112,10 +112,10 @@ __device__ __forceinline__ int pcg_prologue(const PcgArgs &g, int k, double *lds
     int done = 0;
     if (k == 1 && S[4] == 0.0) done = 3;
     else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
-    else if (!(S[0] > 0.0) || !(S[3] > 0.0)) done = 1;  // fp32 underflow (cg_prologue)
-    else if (k - 1 >= g.maxiter) done = 2;
     const double al = S[3] / S[0];
     const double rho = S[3] - 2.0 * al * S[1] + al * al * S[2];
+    if (!done && (!(S[0] > 0.0) || !(S[3] > 0.0) || !(rho > 0.0))) done = 1;  // noise floor (cg_prologue)
+    else if (!done && k - 1 >= g.maxiter) done = 2;
     if (lead) {
       if (k == 1) { g.st->bnorm = rn; g.st->atol = atol; }
       g.st->iter = k - 1;
@@ -292,13 +292,13 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       const double atol = k == 1 ? g.rtol * rn : st_atol;
       if (k == 1 && S[4] == 0.0) done = 3;
       else if (rn < atol || S[4] == 0.0) done = 1;  // exact solution: nothing left to divide
-      // p.Ap or r.z underflowed in fp32 (rtol 0 runs past the representable
-      // residual; A and M are SPD, so only rounding makes them vanish):
-      // nothing left to divide either
-      else if (!(S[0] > 0.0) || !(S[3] > 0.0)) done = 1;
-      else if (k - 1 >= g.maxiter) done = 2;
       const double a_ = S[3] / S[0];
       const double rho = S[3] - 2.0 * a_ * S[1] + a_ * a_ * S[2];
+      // p.Ap, r.z or the recurrence's next r.z not positive: fp32 rounding
+      // at the noise floor (rtol 0 runs past the representable residual; A
+      // and M are SPD, so only rounding makes them vanish): stop there
+      if (!done && (!(S[0] > 0.0) || !(S[3] > 0.0) || !(rho > 0.0))) done = 1;
+      else if (!done && k - 1 >= g.maxiter) done = 2;
       if (blockIdx.x == 0 && blockIdx.y == 0) {
         if (k == 1) { g.st->bnorm = rn; g.st->atol = atol; }
         g.st->iter = k - 1;
@@ -546,7 +546,9 @@ __device__ __forceinline__ cg_f4 cgr_diag_raw(const CgRaw &c, cg_f4 f) {
 // sweeps are separated by workgroup barriers; reductions are fixed-order fp64.
 #define CGS_BX 64
 #define CGS_BY 16
+#ifndef CG_SMALL_PX
 #define CG_SMALL_PX 4096
+#endif
 
 struct CgSmallArgs {
   const float *coef;  // 7 planes, plane stride ps
@@ -817,6 +819,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   const int xcd = lin & 7, tile = xcd * (nt >> 3) + min(xcd, nt & 7) + (lin >> 3);
   const int lane = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(threadIdx.y), band = tile / gridDim.x;
   const int tid = lane + wid * 64;
+  // pipeline role of this wave (A/B, round 2: pairing the roles of two
+  // co-resident blocks differently on the SIMDs, role = wid ^ f(block), was
+  // no faster: 51.5-54 vs 52 us per 1080p launch)
+  const int role = wid;
   const int jc = (tile - band * gridDim.x) * PCG_SWP - 8 + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
   const bool out_lane = lane >= 4 && lane <= 59;
@@ -916,7 +922,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   // rings indexed by (row - ns) mod ring size)
   CgRaw SG[CGS_SGN], SGp[2];
   cg_f4 PO[8], RI[CGS_RIN], PO2[CGS_W2N], XI[CGS_W2N];
-  if (live && wid == 0) {
+  if (live && role == 0) {
     load_raw(ns - 2, SGp[0]);
     load_raw(ns - 1, SGp[1]);
 #pragma unroll
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #pragma unroll
     for (int m = -1; m < CGS_PF - 1; ++m) RI[(m + 16) & (CGS_RIN - 1)] = load_rin(ns + m);
   }
-  if (live && wid == 2) {
+  if (live && role == 2) {
 #pragma unroll
     for (int m = -8; m < CGS_PF2 - 8; ++m) {
       PO2[(m + 16) & (CGS_W2N - 1)] = load_po(ns + m);
@@ -939,7 +945,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (live) {
-    if (wid == 0) {
+    if (role == 0) {
       put_rec(ns - 2, SGp[0]);
       put_rec(ns - 1, SGp[1]);
     }
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #define RSG(d) ((u + (d) + 16) & (CGS_SGN - 1))
 #define RRI(d) ((u + (d) + 16) & (CGS_RIN - 1))
 #define RW2(d) ((u + (d) + 16) & (CGS_W2N - 1))
-    if (wid == 0) {
+    if (role == 0) {
       CGS_STEPS({
         load_raw(n + CGS_PF, SG[RSG(CGS_PF)]);
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
@@ -988,7 +994,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           acc[3] += (double)(c0 * mdot(r, y));
         }
       })
-    } else if (wid == 1) {
+    } else if (role == 1) {
       // Horner, degree 5: g4 = c4 y + c5 B y (row n-3), g3 = c3 y + B g4
       // (n-4), g2 = c2 y + B g3 (n-5), g1 = c1 y + B g2 (n-6) -> LDS
       cg_f4 G4[4] = {zero4, zero4, zero4, zero4}, G3[4] = {zero4, zero4, zero4, zero4};
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           st4(s_g1, n - 6, c1 * yrow(n - 6) + cgr_minv(q, ng));
         }
       })
-    } else if (wid == 2) {
+    } else if (role == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
       CGS_STEPS({
         PO2[RW2(CGS_PF2 - 8)] = load_po(n + CGS_PF2 - 8);
