@@ -427,7 +427,7 @@ __device__ __forceinline__ float wmf_w(const float2 &s, wmf_v2f c01, float, floa
 }
 
 // v from lane ^ lj: DPP for lj = 1, 2 (quad_perm) and 8 (row_ror:8), a
-// ds_bpermute otherwise (lj is a constant once the sort loops are unrolled)
+// ds_bpermute otherwise (lj = 4; 16 and 32 use swap_lane64 below) (lj is a constant once the sort loops are unrolled)
 __device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lj) {
   const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
   int a, b;
@@ -446,6 +446,24 @@ __device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lj) {
   return ((uint64_t)(uint32_t)b << 32) | (uint32_t)a;
 }
 
+// (own, partner) of lane ^ lj for lj = 16 / 32 in unspecified order per lane:
+// v_permlane16_swap / v_permlane32_swap (gfx950) of each 32-bit half with itself
+__device__ __forceinline__ void swap_lane64(uint64_t v, int lj, uint64_t &a, uint64_t &b) {
+  const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+  unsigned alo, blo, ahi, bhi;
+  if (lj == 16) {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+  }
+  a = ((uint64_t)ahi << 32) | alo;
+  b = ((uint64_t)bhi << 32) | blo;
+}
+
 // Bitonic sort of the 64*NPER keys of two lists at once (element e = lane *
 // NPER + r).  Partners at distance >= NPER are in another lane (xor_lane64),
 // the others in the same lane.  The direction of a compare-exchange is a lane
@@ -461,11 +479,25 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
         const int lj = jj / NPER;
         // kk > NPER here: the direction depends on the lane only
         const bool take_min = ((lane & lj) == 0) == (((lane * NPER) & kk) == 0);
+        if (lj == 16 || lj == 32) {
+          // v_permlane{16,32}_swap of a value with itself leaves (own, partner)
+          // in the two outputs, in a lane-dependent order; min / max of the
+          // pair is order-free, so no select of the partner is needed
 #pragma unroll
-        for (int r = 0; r < NPER; ++r) {
-          const uint64_t oa = xor_lane64(ka[r], lj), ob = xor_lane64(kb[r], lj);
-          ka[r] = ((ka[r] < oa) == take_min) ? ka[r] : oa;
-          kb[r] = ((kb[r] < ob) == take_min) ? kb[r] : ob;
+          for (int r = 0; r < NPER; ++r) {
+            uint64_t p0, p1, q0, q1;
+            swap_lane64(ka[r], lj, p0, p1);
+            swap_lane64(kb[r], lj, q0, q1);
+            ka[r] = ((p0 < p1) == take_min) ? p0 : p1;
+            kb[r] = ((q0 < q1) == take_min) ? q0 : q1;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < NPER; ++r) {
+            const uint64_t oa = xor_lane64(ka[r], lj), ob = xor_lane64(kb[r], lj);
+            ka[r] = ((ka[r] < oa) == take_min) ? ka[r] : oa;
+            kb[r] = ((kb[r] < ob) == take_min) ? kb[r] : ob;
+          }
         }
       } else {
 #pragma unroll

@@ -264,10 +264,11 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
   __shared__ float s_ab[2];
   const int tid = threadIdx.x + threadIdx.y * 64;
   int st_done = 0;
-  double st_atol = 0.0;
+  double st_atol = 0.0, st_rho = 0.0;
   if (tid == 0) {
     st_done = g.st->done;
     st_atol = g.st->atol;
+    if (k >= 2) st_rho = g.st->rho[(k - 1) & 1];  // launch k-1's recurrence value of r.z
   }
   double S[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (!FIRST) {
@@ -298,7 +299,13 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       // at the noise floor (rtol 0 runs past the representable residual; A
       // and M are SPD, so only rounding makes them vanish): stop there
       if (!done && (!(S[0] > 0.0) || !(S[3] > 0.0) || !(rho > 0.0))) done = 1;
-      else if (!done && k - 1 >= g.maxiter) done = 2;
+      // the r.z the last sweep formed (S[3]) off the recurrence's prediction
+      // of it by more than 10 % (they agree to ~1e-6 above the noise floor):
+      // conjugacy is lost, restart with beta = 0 (a preconditioned steepest
+      // descent step never increases the A-norm error) instead of letting
+      // the recurrence drive the iterate away
+      const bool drift = k >= 2 && !(fabs(S[3] - st_rho) <= 0.1 * S[3]);
+      if (!done && k - 1 >= g.maxiter) done = 2;
       if (blockIdx.x == 0 && blockIdx.y == 0) {
         if (k == 1) { g.st->bnorm = rn; g.st->atol = atol; }
         g.st->iter = k - 1;
@@ -307,7 +314,7 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
         if (done) g.st->done = done;
       }
       al = (float)a_;
-      be = (float)(rho / S[3]);
+      be = drift ? 0.f : (float)(rho / S[3]);
     }
     if (FIRST && blockIdx.x == 0 && blockIdx.y == 0) {
       g.st->iter = 0;

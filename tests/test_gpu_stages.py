@@ -292,3 +292,34 @@ def test_solve_synthetic_both_cg_paths(H, W):
     o.solver = "pcg"
     x = flat(o._solve_linear_system(A, b, (H, W, 2)))
     assert np.linalg.norm(x - xs) <= 2e-2 * np.linalg.norm(xs), np.linalg.norm(x - xs) / np.linalg.norm(xs)
+
+
+@pytest.mark.parametrize("H,W", [(40, 56), (64, 96), (150, 200)])
+def test_solve_rtol0_stops_at_noise_floor(H, W):
+    """rtol 0 runs CG past the fp32-representable residual: the solve must stop
+    there (prologue test on p.Ap, r.z and the recurrence's next r.z) or
+    restart (beta = 0) when the r.z a sweep formed departs from the
+    recurrence's prediction, with a finite iterate near direct-solve accuracy
+    (1e-3; the rtol 1e-6 solves of test_solve_synthetic_both_cg_paths reach
+    1e-4), never return NaN or diverge (both happened before the test
+    existed: NaN at 1080p, 1.6e18 for 'pcg' at 64x96; profiles/r2t_cgs_ab.md).
+    Covers k_cg_small (40x56), the fused k_cgs launches and 'pcg' (k_cg)."""
+    from optical_flow.methods.config import load_of_method
+    from scipy.sparse.linalg import spsolve
+    A, b = _spd_flow_system(H, W, seed=H + W)
+    xr = spsolve(A.tocsc(), b)
+    o = load_of_method("classic+nl-fast")
+    o.backslash_rtol = 0.0
+    o.backslash_maxiter = 3000
+    o.pcg_rtol = 0.0
+    o.pcg_maxiter = 3000
+
+    def flat(x):
+        return np.concatenate([x[..., 0].ravel(order="F"), x[..., 1].ravel(order="F")])
+
+    for solver in ("backslash", "pcg"):
+        o.solver = solver
+        x = flat(o._solve_linear_system(A, b, (H, W, 2)))
+        assert np.all(np.isfinite(x)), solver
+        err = np.linalg.norm(x - xr) / np.linalg.norm(xr)
+        assert err <= 1e-3, (solver, err)
