@@ -426,8 +426,9 @@ __device__ __forceinline__ float wmf_w(const float2 &s, wmf_v2f c01, float, floa
   return fmaxf(__builtin_amdgcn_exp2f(e * e * nk) * s.y, 1e-10f);
 }
 
-// v from lane ^ lj: DPP for lj = 1, 2 (quad_perm) and 8 (row_ror:8), a
-// ds_bpermute otherwise (lj = 4; 16 and 32 use swap_lane64 below) (lj is a constant once the sort loops are unrolled)
+// v from lane ^ lj: DPP for lj = 1, 2 (quad_perm), 4 (row_half_mirror then
+// quad_perm) and 8 (row_ror:8), a ds_bpermute otherwise (16 and 32 use
+// swap_lane64 below) (lj is a constant once the sort loops are unrolled)
 __device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lj) {
   const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
   int a, b;
@@ -440,6 +441,9 @@ __device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lj) {
   } else if (lj == 8) {
     a = __builtin_amdgcn_mov_dpp(lo, 0x128, 0xf, 0xf, false);
     b = __builtin_amdgcn_mov_dpp(hi, 0x128, 0xf, 0xf, false);
+  } else if (lj == 4) {  // row_half_mirror (l ^ 7), then quad_perm [3,2,1,0] (l ^ 3)
+    a = __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(lo, 0x141, 0xf, 0xf, false), 0x1B, 0xf, 0xf, false);
+    b = __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(hi, 0x141, 0xf, 0xf, false), 0x1B, 0xf, 0xf, false);
   } else {
     return __shfl_xor(v, lj);
   }
