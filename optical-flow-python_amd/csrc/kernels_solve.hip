@@ -958,6 +958,11 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     }
     __syncthreads();
     CGS_T0
+    // issue priority for the pace-setting roles (loads + stage A, and z / p /
+    // q) over the Horner and T waves they share a SIMD with: 52 -> 50 us
+    // per 1080p launch (A/B, profiles/r2z_cgs_setprio_ab.log; wave 0
+    // alone: 51.3)
+    if (role == 0 || role == 2) __builtin_amdgcn_s_setprio(2);
     // each wave runs its own role's loop (registers of one role only), one
     // block barrier per row step in every role (same step count)
 #define CGS_STEPS(...)                                                    \
