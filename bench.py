@@ -55,7 +55,11 @@ KERNEL_BYTES_PER_PX = {
     "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ
     "wmf": 8 + 4 + 12 + 8,                 # uv, occ, Lab -> uv
     "rof_iters": 4 + 8 + 8,                # im, p -> p per channel, ROF_K iterations per launch
+    "sor_sweep": 36 + 8 + 8,               # 7 coef + 2 rhs planes, x read + write (52 B/px/sweep)
 }
+# VALU issue peak (MI355X_MICROARCH.md: a wave issues one VALU instruction per
+# 2 cycles per SIMD; 256 CUs x 4 SIMDs at 2.4 GHz): wave-instructions / s
+VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9
 
 
 def parse():
@@ -168,20 +172,47 @@ def cpu_baseline(args):
                       f"synth_pair({args.height},{args.width},0): {dt:.2f} s, scaled x{scale:.1f} by pixel count"}
 
 
-def load_pmc_traffic(kernel, which="finest"):
-    """HBM bytes per launch of `kernel` (2*FETCH_SIZE + WRITE_SIZE) from the
-    committed rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
-    tools/prof_summary.py --traffic): averaged over all launches ("all") or
-    over the finest level's launches ("finest")."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def load_pmc(kernel):
+    """The kernel's record in the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/prof_summary.py --traffic
+    from tools/profile.sh's counter passes; shipped to the GPU box), or {}."""
     try:
-        d = json.load(open(p))
-        rec = d.get(kernel, {})
-        return rec.get("hbm_bytes_per_launch_all" if which == "all" else "hbm_bytes_per_launch")
-    except Exception:
+        return json.load(open(PMC_FILE)).get(kernel, {}) or {}
+    except (OSError, ValueError):
+        return {}
+
+
+def load_pmc_traffic(kernel, which="finest"):
+    """HBM bytes per launch of `kernel` (2*FETCH_SIZE + WRITE_SIZE, profiles/
+    pmc_traffic.json): averaged over all launches ("all") or over the finest
+    level's launches ("finest")."""
+    return load_pmc(kernel).get("hbm_bytes_per_launch_all" if which == "all" else "hbm_bytes_per_launch")
+
+
+def wmf_compute_roofline(per_level):
+    """The weighted median is VALU-issue bound, not HBM bound (SURVEY.md
+    §8d): VALU wave-instructions per finest-level launch (SQ_INSTS_VALU, PMC
+    pass of tools/profile.sh) / that launch's mean duration in the isolated
+    replay, against the chip's VALU issue rate (VALU_ISSUE_PEAK)."""
+    rec = load_pmc("wmf")
+    lv = [(px, r) for (n, px), r in per_level.items() if n == "wmf"]
+    if not lv:
         return None
+    px, r = max(lv, key=lambda t: t[0])
+    ms = r["ms_total"] / r["launches"]
+    out = {"bound": "valu-issue", "px_per_launch": px, "mean_launch_ms": round(ms, 4),
+           "mpx_per_ms": round(px / 1e6 / ms, 3), "alg_bytes_per_px": KERNEL_BYTES_PER_PX["wmf"],
+           "hbm_frac": round(KERNEL_BYTES_PER_PX["wmf"] * px / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    vi = rec.get("valu_insts_per_launch")
+    if vi and rec.get("grid") == px:
+        ach = vi / (ms * 1e-3)
+        out.update({"valu_insts_per_launch": vi, "valu_insts_per_px": round(vi * 64 / px, 1),
+                    "achieved": round(ach / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                    "unit": "G wave-instr/s", "frac": round(ach / VALU_ISSUE_PEAK, 4)})
+    return out
 
 
 def roofline_of(ktimes, per_level):
@@ -250,18 +281,24 @@ def profiled_replay(ctx, lib, P0, pairs, lanes):
 # bytes, over the time of every kernel of the loop
 INNER_BYTES = {"partial_deriv_hermite": 48, "partial_deriv_bspline": 44, "partial_deriv_bilinear": 44,
                "flow_operator": 56, "update_occ": 24}
-INNER_TIME_ONLY = ("pcg_small", "pcg_check", "axpy_diff", "add_update", "sor_sweep")
+INNER_TIME_ONLY = ("pcg_small", "pcg_check", "cg_update", "cg_finalize", "axpy_diff", "add_update", "sor_init",
+                   "sor_final")
 
 
 def inner_loop_of(ktimes, per_level):
-    """bytes: the per-px figures above x the pixels of every launch, and
-    76 B x the pixels of every CG launch that did work (pcg_iter.active;
-    the one-workgroup coarse-level solves, pcg_small, count time but no
-    bytes: conservative); time: HIP events of all those kernels."""
+    """bytes: the per-px figures above x the pixels of every launch, 76 B x
+    the pixels of every CG launch that did work (pcg_iter.active) and 52 B x
+    the pixels of every SOR sweep; the one-workgroup coarse-level solves
+    (pcg_small) and the 'backslash' residual replacement / finalisation
+    count time but no bytes (conservative); time: HIP events of all those
+    kernels."""
     byt, ms = 0.0, 0.0
     for name, rec in ktimes.items():
         if name in INNER_BYTES:
             byt += INNER_BYTES[name] * rec["px"]
+            ms += rec["ms_total"]
+        elif name == "sor_sweep":
+            byt += KERNEL_BYTES_PER_PX["sor_sweep"] * rec["px"]
             ms += rec["ms_total"]
         elif name == "pcg_iter":
             ms += rec["ms_total"]
@@ -273,19 +310,32 @@ def inner_loop_of(ktimes, per_level):
     if ms <= 0:
         return None
     ach = byt / (ms * 1e-3) / 1e9
-    fine = max((px for (n, px) in per_level if n == "pcg_iter"), default=None)
+    fine = max((px for (n, px) in per_level if n in ("pcg_iter", "sor_sweep")), default=None)
     out = {"bytes_per_step": round(byt), "kernel_ms_per_step": round(ms, 3), "achieved": round(ach, 1),
            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-           "formula": "sum N*(48+56+24) per warp + 76*N*K_pcg; time of warp, assembly, update, CG kernels"}
+           "formula": "sum N*(48|44 + 56 + 24) per warp + 76*N*K_pcg | 52*N*K_sor; time of warp, assembly, update, "
+                      "solver kernels"}
     if fine:
         b2 = sum(INNER_BYTES[n] * r["px"] for (n, px), r in per_level.items() if px == fine and n in INNER_BYTES)
         b2 += KERNEL_BYTES_PER_PX["pcg_iter"] * per_level.get(("pcg_iter.active", fine), {"px": 0})["px"]
+        b2 += KERNEL_BYTES_PER_PX["sor_sweep"] * per_level.get(("sor_sweep", fine), {"px": 0})["px"]
         m2 = sum(r["ms_total"] for (n, px), r in per_level.items() if px == fine and
-                 (n in INNER_BYTES or n == "pcg_iter" or n in INNER_TIME_ONLY))
+                 (n in INNER_BYTES or n in ("pcg_iter", "sor_sweep") or n in INNER_TIME_ONLY))
         if m2 > 0:
             a2 = b2 / (m2 * 1e-3) / 1e9
             out["finest"] = {"px": fine, "achieved": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4)}
     return out
+
+
+def kms(kt, pairs, top=14):
+    return {k: round(v["ms_total"] / pairs, 3) for k, v in
+            sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])[:top] if not k.endswith(".active")}
+
+
+def metric_name(args):
+    tag = {"classic+nl-fast": "Classic+NL-fast", "hs": "HS", "classic-c": "Classic-C"}.get(args.method, args.method)
+    solver = f" ({args.solver})" if args.solver else ""
+    return f"image-pairs/sec at {args.width}x{args.height} {tag}{solver} (+ ms/pyramid-level, AEPE)"
 
 
 def main():
@@ -365,7 +415,7 @@ def main():
     sd = st.as_dict()
 
     roofline = None
-    ktimes = {}
+    ktimes, kt_iso = {}, {}
     pcg_levels = None
     inner = None
     if not args.no_profile:
@@ -379,6 +429,7 @@ def main():
         # kernel's duration is its own, not stretched by another lane's
         # kernels sharing the CUs (profiles/: rocprofv3 of bench.py --lanes 1)
         kt1, pl1 = profiled_replay(ctx, lib, P0, args.pairs, 1)
+        kt_iso = kt1
         roofline = roofline_of(kt1, pl1)
         if roofline is not None:
             roofline["replay"] = "isolated: lanes=1 over the step's pairs"
@@ -390,13 +441,14 @@ def main():
                 "achieved": rc["achieved"], "frac": rc["frac"], "mean_launch_ms": rc["mean_launch_ms"],
                 "inner_loop_frac": conc["frac"] if conc else None}
             roofline["inner_loop"] = inner
+            roofline["wmf"] = wmf_compute_roofline(pl1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
 
     if rank == 0:
         line = {
-            "metric": "image-pairs/sec at 1920x1080 Classic+NL-fast (+ ms/pyramid-level, AEPE)",
+            "metric": metric_name(args),
             "value": round(value, 4), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -417,9 +469,11 @@ def main():
             "aepe_gt": round(aepe, 5), "solver_iters_total": sd["solver_iters_total"],
             "solver_iters_max": sd["solver_iters_max"], "solves": sd["solves"],
             "pcg_per_level": pcg_levels,
-            "kernel_ms_per_pair": {k: round(v["ms_total"] / args.pairs, 3) for k, v in
-                                   sorted(ktimes.items(), key=lambda kv: -kv[1]["ms_total"])[:12]
-                                   if not k.endswith(".active")},
+            # HIP-event kernel time per pair: isolated = the lanes=1 replay
+            # (sums to <= the serial pair time); concurrent = the lanes replay
+            # as timed, where durations include co-running lanes' kernels
+            "kernel_ms_per_pair_isolated": kms(kt_iso, args.pairs),
+            "kernel_ms_per_pair_concurrent": kms(ktimes, args.pairs),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OF_ABI_VERSION 1
+#define OF_ABI_VERSION 2
 
 /* status codes */
 #define OF_OK 0
@@ -201,10 +201,12 @@ int of_pairs_run(of_ctx *ctx, int nslots, const of_params *params, int lanes, of
  * npairs caller-owned (H, W, C) uint8 frame pairs (C = 1 or 3), writes each
  * pair's flow as planar 2 x H x W fp32 into out_uv[k].  `lanes` pairs in
  * flight as in of_pairs_run; per lane the H2D of pair j+1's bytes and the
- * D2H of pair j-1's flow overlap pair j's kernels (pinned double buffers, a
- * copy stream).  The flows also stay on the device in slots 0..npairs-1
- * (of_pair_download, of_rccl_gather_flows).  Results equal of_pairs_run on
- * the same frames (bitwise, independent of `lanes`). */
+ * D2H of pair j-1's flow overlap pair j's kernels (pinned double buffers, one
+ * copy stream shared by the lanes).  The flows also stay on the device in
+ * slots 0..npairs-1 (of_pair_download, of_rccl_gather_flows); frames an
+ * earlier of_pair_upload left in those slots are released (re-upload before
+ * of_pair_run / of_pairs_run).  Results equal of_pairs_run on the same frames
+ * (bitwise, independent of `lanes`). */
 int of_pairs_run_host(of_ctx *ctx, int npairs, const uint8_t *const *im1, const uint8_t *const *im2, int H, int W,
                       int C, const of_params *params, int lanes, float *const *out_uv, of_stats *stats);
 /* D2H of a slot's flow (planar 2 x H x W) */
@@ -237,16 +239,23 @@ int of_solver_geometry(int H, int W, int solver, of_cg_geometry *out);
  * base.py:87-172) is followed by an fp64 evaluation of its TRUE relative
  * residual ||b - A x|| / ||b|| from the fp32 operator; records keep the
  * solver's own estimate beside it (CG: the recurrence residual; SOR: the
- * last sweep's ||dx|| / ||x||).  Enabling clears the log; at most 4096
- * records per context.  Diagnostic only: adds two small launches per solve. */
+ * last sweep's ||dx|| / ||x||).  true_rel is the residual of the solver's
+ * iterate ('backslash': x_hi + x_lo summed in fp64 after its residual
+ * replacement, the quantity its stopping test approximates), true_rel_out
+ * that of the fp32 x it returns (the same for 'pcg' and 'sor'; for
+ * 'backslash' it includes the rounding of the solution to fp32, whose
+ * residual alone is ~2e-6 on Classic+NL robust stages, tools/fp32_floor.py).
+ * Enabling clears the log; at most 4096 records per context.  Diagnostic
+ * only: adds small launches per solve. */
 typedef struct of_solve_record {
   int32_t h, w;
   int32_t solver;   /* enum of_solver */
   int32_t iters;    /* CG iterations / SOR sweeps */
   int32_t done;     /* 1 converged, 2 iteration limit, 3 zero rhs */
   int32_t pad_;
-  double true_rel;  /* ||b - A x|| / ||b||, fp64 */
+  double true_rel;      /* ||b - A x|| / ||b||, fp64, of the solver's iterate */
   double est_rel;
+  double true_rel_out;  /* ... of the returned fp32 x */
 } of_solve_record;
 int of_set_solve_log(of_ctx *ctx, int enable);
 int of_solve_log(of_ctx *ctx, int max, of_solve_record *out, int *n);

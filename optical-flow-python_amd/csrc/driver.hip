@@ -107,9 +107,14 @@ struct Slot {
 
 // of_pairs_run_host staging of one lane: two pinned input/output buffers and
 // two device frame buffers, so pair j+1's bytes go up on the copy stream and
-// pair j-1's flow comes down while pair j computes
+// pair j-1's flow comes down while pair j computes.  All lanes share the
+// parent context's copy stream (`copy`, owned when own_copy): lanes + 1
+// streams in all, within GPU_MAX_HW_QUEUES (4) for lanes <= 3.  No copy waits
+// on a lane's kernels inside the stream (the helper threads wait on the host),
+// so one lane's copies never queue behind another lane's pair.
 struct HostStage {
   hipStream_t copy = nullptr;
+  bool own_copy = false;
   uint8_t *pin_in[2] = {nullptr, nullptr}, *d_in[2] = {nullptr, nullptr};
   float *pin_out[2] = {nullptr, nullptr};
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_conv[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
@@ -158,6 +163,8 @@ struct of_ctx {
     double est;
   };
   std::vector<SolveLog> slog_rec;
+  int slog_idx = -1;       // log entry of the solve being issued (-1: none)
+  bool slog_iter = false;  // ... whose iterate residual the solver logged itself
   double *d_rpart = nullptr, *d_rlog = nullptr;
   uint32_t *d_mm = nullptr;  // 32 min/max pairs
   double *d_norm = nullptr, *h_norm = nullptr;
@@ -587,6 +594,7 @@ template <typename Enq>
 int run_fed(of_ctx *c, volatile CgFlag *f, int nmax, int depth, Enq enqueue_iter) {
   f->done = 0;
   f->iter = 0;
+  f->upd = 0;
   f->k = -1;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   int enq = 0;
@@ -711,6 +719,31 @@ int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
   return g->blocks <= PCG_MAX_BLOCKS ? OF_OK : OF_ENOTSUP;
 }
 
+// launches between 'backslash' residual-replacement offers (k_cg_update)
+#define CG_UPD_EVERY 4
+
+// fp64 true residual ||b - A (x [+ x_hi])||^2 and ||b||^2 into out[0..1]
+// (solve log)
+void log_resid(of_ctx *c, const Img &coef, const F2 &b, const F2 &x, const F2 *xh, double *out) {
+  Grid2 g = grid2(b.H, b.W, PCG_MAX_BLOCKS);
+  launch(c, "resid", k_resid_part, g.grid, g.block, 0, (const float *)coef.p, coef.ps(), (const float2 *)b.p,
+         (const float2 *)x.p, xh ? (const float2 *)xh->p : nullptr, (const PcgState *)(xh ? c->d_state : nullptr),
+         b.H, b.W, b.P, c->d_rpart);
+  launch(c, "resid", k_resid_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_rpart, g.nblocks, out);
+}
+
+// end of a 'backslash' CG solve: with the solve log on, the true residual of
+// the solver's iterate x_hi + x_lo (fp64 sum); then x = fl32(x_hi + x_lo)
+void finish_backslash(of_ctx *c, const Img &coef, const F2 &b, const F2 &x, const F2 &xh) {
+  if (c->slog_idx >= 0) {
+    log_resid(c, coef, b, x, &xh, c->d_rlog + 4 * c->slog_idx);
+    c->slog_iter = true;
+  }
+  Grid2 g = grid2(x.H, x.W);
+  launch(c, "cg_finalize", k_cg_finalize, g.grid, g.block, 0, x.p, (const float2 *)xh.p, (const PcgState *)c->d_state,
+         x.H, x.W, x.P);
+}
+
 SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
   const int H = b.H, W = b.W;
   c->cur_px = (double)H * W;
@@ -735,6 +768,11 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     SolveResult res{0, 0, 0.0};
     res.slot = slot;
     res.px = (double)H * W;
+    // 'backslash': one residual replacement at ||r|| < sqrt(rtol) ||b||
+    // (k_cg_update), x_hi beside the solve's x
+    const double rtol = block ? P->exact_rtol : P->pcg_rtol;
+    const double upd_rel = block && rtol > 0 ? std::sqrt(rtol) : 0.0;
+    const F2 xh = block ? new_f2(c, H, W) : F2{};
     // coarse levels: the whole solve in one workgroup (k_cg_small)
     if ((double)H * W <= CG_SMALL_PX) {
       CgSmallArgs a;
@@ -754,13 +792,16 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
       a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
       for (int i = 0; i < 8; ++i) a.poly[i] = poly[i];
       a.st = c->d_state;
+      a.xh = xh.p;
+      a.upd_rel = upd_rel;
       launch(c, "pcg_small", block ? k_cg_small<CG_DEG, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY), 0,
              a);
+      if (block) finish_backslash(c, coef, b, x, xh);
       HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
       return res;
     }
     res.name = "pcg_iter";
-    // 'backslash': k_cgs (the degree-3 iteration with its stages split over a
+    // 'backslash': k_cgs (the degree-5 iteration with its stages split over a
     // block's 4 waves); 'pcg': scipy's Jacobi CG in k_cg
     const bool split = block;
     of_cg_geometry geo;
@@ -781,8 +822,11 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     a.ps = ps;
     a.nb = geo.blocks;
     a.st = c->d_state;
-    a.rtol = block ? P->exact_rtol : P->pcg_rtol;
+    a.rtol = rtol;
     a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
+    a.xh = xh.p;
+    a.upd_part = block ? c->d_partials + 15 * PCG_MAX_BLOCKS : nullptr;
+    a.upd_rel = upd_rel;
     HIPCHK(hipMemsetAsync(c->d_state, 0, sizeof(PcgState), c->stream));
     auto args_k = [&](int k) {
       PcgArgs ak = a;
@@ -797,7 +841,12 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     };
     for (int i = 0; i < 8; ++i) a.poly[i] = poly[i];
     a.hflag = c->d_flag + slot;
-    const int enq = run_fed(c, c->h_flag + slot, a.maxiter + 1, 3, [&](int k) {
+    volatile CgFlag *hf = c->h_flag + slot;
+    const int enq = run_fed(c, hf, a.maxiter + 1, 3, [&](int k) {
+      // the replacement is offered every CG_UPD_EVERY launches until the
+      // host sees that it ran (it acts at most once; extra offers are no-ops)
+      if (upd_rel > 0 && k >= 2 * CG_UPD_EVERY && k % CG_UPD_EVERY == 0 && !hf->upd)
+        launch(c, "cg_update", k_cg_update, grid, blk, 0, args_k(k), k);
       const bool odd = W & 1;
       auto kern = split ? (k == 0 ? (odd ? k_cgs<true, true> : k_cgs<true, false>)
                                   : (odd ? k_cgs<false, true> : k_cgs<false, false>))
@@ -806,6 +855,7 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
     launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
+    if (block) finish_backslash(c, coef, b, x, xh);
     HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     return res;
   }
@@ -859,14 +909,16 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
 // _solve_linear_system; with the solve log on, followed by the fp64 true
 // residual of the final x (diagnostic, off by default)
 SolveResult solve(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
+  const int idx = c->slog && c->slog_rec.size() < OF_SLOG_MAX ? (int)c->slog_rec.size() : -1;
+  c->slog_idx = idx;
+  c->slog_iter = false;
   const SolveResult r = solve_impl(c, P, coef, b, x);
-  if (c->slog && c->slog_rec.size() < OF_SLOG_MAX) {
-    const int idx = (int)c->slog_rec.size();
-    Grid2 g = grid2(b.H, b.W, PCG_MAX_BLOCKS);
-    launch(c, "resid", k_resid_part, g.grid, g.block, 0, (const float *)coef.p, coef.ps(), (const float2 *)b.p,
-           (const float2 *)x.p, b.H, b.W, b.P, c->d_rpart);
-    launch(c, "resid", k_resid_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_rpart, g.nblocks,
-           c->d_rlog + 2 * idx);
+  c->slog_idx = -1;
+  if (idx >= 0) {
+    // residual of the returned fp32 x; also the iterate's unless the solver
+    // logged that itself (finish_backslash)
+    log_resid(c, coef, b, x, nullptr, c->d_rlog + 4 * idx + 2);
+    if (!c->slog_iter) log_resid(c, coef, b, x, nullptr, c->d_rlog + 4 * idx);
     c->slog_rec.push_back({b.H, b.W, P->solver, r.slot, r.iters, r.done, r.rel});
   }
   return r;
@@ -969,12 +1021,13 @@ struct LevelIn {
   Img guide;  // gc planes or p == nullptr
 };
 
-// Lanes mode (of_pairs_run): a phase on a level of >= big_px pixels (the
-// full-size preprocessing and every fine CG solve) holds the lanes' shared
-// token until its GPU work has drained, so at most one pair at a time streams
-// a fine CG working set (1080p: ~190 MB, most of the 256 MB Infinity Cache)
-// and two lanes' 512-block CG launches never interleave.  Outside lanes
-// mode: no-op.
+// Lanes mode (of_pairs_run, of_pairs_run_host): a linear solve on a level of
+// >= big_px pixels (solve_tok below; nothing else takes the token) holds the
+// lanes' shared token until its GPU work has drained, so at most one pair at a
+// time streams a fine CG working set (1080p: ~190 MB, most of the 256 MB
+// Infinity Cache) and two lanes' 512-block CG launches never interleave.
+// Preprocessing, warps, assembly and the weighted median of fine levels run
+// unserialised.  Outside lanes mode: no-op.
 struct BigPhase {
   of_ctx *c;
   bool held = false;
@@ -1364,7 +1417,7 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipMalloc(&c->d_partials, sizeof(double) * 16 * PCG_MAX_BLOCKS));
     HIPCHK(hipMalloc(&c->d_sor_sync, OF_SOR_SYNC_BYTES));
     HIPCHK(hipMalloc(&c->d_rpart, sizeof(double) * 2 * PCG_MAX_BLOCKS));
-    HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 2 * OF_SLOG_MAX));
+    HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 4 * OF_SLOG_MAX));
     HIPCHK(hipFuncSetAttribute((const void *)k_sor_lex, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
@@ -1463,8 +1516,8 @@ int of_solve_log(of_ctx *c, int max, of_solve_record *out, int *n) {
   *n = m;
   const int k = std::min(m, max);
   if (k > 0) {
-    std::vector<double> h(2 * (size_t)k);
-    HIPCHK(hipMemcpy(h.data(), c->d_rlog, sizeof(double) * 2 * k, hipMemcpyDeviceToHost));
+    std::vector<double> h(4 * (size_t)k);
+    HIPCHK(hipMemcpy(h.data(), c->d_rlog, sizeof(double) * 4 * k, hipMemcpyDeviceToHost));
     for (int e = 0; e < k; ++e) {
       const auto &l = c->slog_rec[e];
       of_solve_record &o = out[e];
@@ -1474,7 +1527,8 @@ int of_solve_log(of_ctx *c, int max, of_solve_record *out, int *n) {
       o.solver = l.solver;
       o.iters = l.iters;
       o.done = l.done;
-      o.true_rel = h[2 * e + 1] > 0 ? std::sqrt(h[2 * e] / h[2 * e + 1]) : 0.0;
+      o.true_rel = h[4 * e + 1] > 0 ? std::sqrt(h[4 * e] / h[4 * e + 1]) : 0.0;
+      o.true_rel_out = h[4 * e + 3] > 0 ? std::sqrt(h[4 * e + 2] / h[4 * e + 3]) : 0.0;
       o.est_rel = l.est;
     }
   }
@@ -1702,10 +1756,13 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
 }
 
 namespace {
-void stage_alloc(of_ctx *l, size_t in_bytes, size_t out_floats) {
+void stage_alloc(of_ctx *l, of_ctx *parent, size_t in_bytes, size_t out_floats) {
   if (!l->hs) {
     l->hs = new HostStage();
-    HIPCHK(hipStreamCreateWithFlags(&l->hs->copy, hipStreamNonBlocking));
+    if (l == parent) {
+      HIPCHK(hipStreamCreateWithFlags(&l->hs->copy, hipStreamNonBlocking));
+      l->hs->own_copy = true;
+    }
     for (int b = 0; b < 2; ++b) {
       HIPCHK(hipEventCreateWithFlags(&l->hs->ev_in[b], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&l->hs->ev_conv[b], hipEventDisableTiming));
@@ -1713,6 +1770,7 @@ void stage_alloc(of_ctx *l, size_t in_bytes, size_t out_floats) {
     }
   }
   HostStage &h = *l->hs;
+  if (!h.own_copy) h.copy = parent->hs->copy;
   if (h.cap_in < in_bytes) {
     for (int b = 0; b < 2; ++b) {
       HIPCHK(hipEventSynchronize(h.ev_in[b]));
@@ -1737,7 +1795,9 @@ void stage_alloc(of_ctx *l, size_t in_bytes, size_t out_floats) {
 void stage_free(of_ctx *l) {
   if (!l->hs) return;
   HostStage &h = *l->hs;
-  if (h.copy) hipStreamSynchronize(h.copy);
+  for (int b = 0; b < 2; ++b)
+    for (hipEvent_t e : {h.ev_in[b], h.ev_out[b]})
+      if (e) hipEventSynchronize(e);
   for (int b = 0; b < 2; ++b) {
     if (h.pin_in[b]) hipHostFree(h.pin_in[b]);
     if (h.pin_out[b]) hipHostFree(h.pin_out[b]);
@@ -1745,7 +1805,10 @@ void stage_free(of_ctx *l) {
     for (hipEvent_t e : {h.ev_in[b], h.ev_conv[b], h.ev_out[b]})
       if (e) hipEventDestroy(e);
   }
-  if (h.copy) hipStreamDestroy(h.copy);
+  if (h.own_copy && h.copy) {
+    hipStreamSynchronize(h.copy);
+    hipStreamDestroy(h.copy);
+  }
   delete l->hs;
   l->hs = nullptr;
 }
@@ -1768,12 +1831,17 @@ void run_host_lane(of_ctx *c, of_ctx *l, int first, int step, int npairs, const 
     HIPCHK(hipEventSynchronize(h.ev_in[b]));  // pinned buffer b free (its last H2D done)
     memcpy(h.pin_in[b], im1[k], nb);
     memcpy(h.pin_in[b] + nb, im2[k], nb);
-    HIPCHK(hipStreamWaitEvent(h.copy, h.ev_conv[b], 0));  // device buffer b no longer read
+    HIPCHK(hipEventSynchronize(h.ev_conv[b]));  // device buffer b no longer read (pair j-2 done)
     HIPCHK(hipMemcpyAsync(h.d_in[b], h.pin_in[b], 2 * nb, hipMemcpyHostToDevice, h.copy));
     HIPCHK(hipEventRecord(h.ev_in[b], h.copy));
   };
+  // pair j's flow: wait for its kernels on the host, then D2H on the shared
+  // copy stream into pinned buffer b and out to the caller
   auto finish = [&](int j) {
     const int b = j & 1;
+    HIPCHK(hipEventSynchronize(h.ev_conv[b]));
+    HIPCHK(hipMemcpyAsync(h.pin_out[b], c->slots[ks[j]].uv, sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
+    HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
     HIPCHK(hipEventSynchronize(h.ev_out[b]));
     memcpy(out_uv[ks[j]], h.pin_out[b], sizeof(float) * nu);
   };
@@ -1817,13 +1885,9 @@ void run_host_lane(of_ctx *c, of_ctx *l, int first, int step, int npairs, const 
       throw;
     }
     HIPCHK(hipEventRecord(h.ev_conv[b], l->stream));  // frames of buffer b consumed, flow k complete
-    HIPCHK(hipStreamWaitEvent(h.copy, h.ev_conv[b], 0));
-    HIPCHK(hipMemcpyAsync(h.pin_out[b], s.uv, sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
-    HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
   }
   join_io();
   if (!ks.empty()) finish((int)ks.size() - 1);
-  HIPCHK(hipStreamSynchronize(h.copy));
 }
 }  // namespace
 
@@ -1849,6 +1913,16 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
       HIPCHK(hipMalloc(&s.uv, sizeof(float) * nu));
       s.cap_uv = nu;
     }
+    // the slot now holds this batch's flow; frames of an earlier
+    // of_pair_upload (possibly of another size) are dropped so that
+    // of_pair_run / of_pairs_run refuse the slot until it is re-uploaded
+    if (s.rgb1 || s.rgb2) {
+      HIPCHK(hipStreamSynchronize(c->stream));
+      hipFree(s.rgb1);
+      hipFree(s.rgb2);
+      s.rgb1 = s.rgb2 = nullptr;
+      s.cap_rgb = 0;
+    }
     s.H = H;
     s.W = W;
     s.C = C;
@@ -1860,7 +1934,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
     REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
     c->lanes.push_back(l);
   }
-  for (int li = 0; li < lanes; ++li) stage_alloc(li ? c->lanes[li - 1] : c, 2 * (size_t)H * W * C, nu);
+  for (int li = 0; li < lanes; ++li) stage_alloc(li ? c->lanes[li - 1] : c, c, 2 * (size_t)H * W * C, nu);
   if (lanes == 1) {
     run_host_lane(c, c, 0, 1, npairs, im1, im2, H, W, C, P, out_uv, st);
   } else {

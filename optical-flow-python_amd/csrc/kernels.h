@@ -45,7 +45,7 @@ struct CgFlag {
   int k;      // last launch whose prologue ran
   int done;   // PcgState::done once decided
   int iter;
-  int pad_;
+  int upd;    // the 'backslash' solve's residual replacement (k_cg_update) has run
 };
 
 struct PcgState {
@@ -57,6 +57,9 @@ struct PcgState {
   int iter;
   int done;         // 0 running, 1 converged, 2 maxiter, 3 zero rhs
   int maxiter;
-  int pad_;
+  // 'backslash' residual replacement: index of the CG launch that follows
+  // the k_cg_update that acted (0: none yet).  That launch starts x_lo from
+  // 0 and takes r.r from the update; x = x_hi + x_lo from then on.
+  int upd_k;
   double xnorm2, dnorm2;  // SOR
 };

@@ -97,6 +97,12 @@ struct PcgArgs {
   double rtol;
   int maxiter;
   float poly[8];  // k_cgs: M^-1 = (poly[0] + poly[1] B + ... + poly[CG_DEG] B^CG_DEG) D^-1
+  // 'backslash' residual replacement (k_cg_update; null / 0 for 'pcg'):
+  // x_hi (the iterate at the replacement), the replacement's per-block r.r
+  // partials, and the relative residual at which it acts
+  float2 *xh;
+  double *upd_part;
+  double upd_rel;
 };
 
 // the shared prologue: returns 1 when the solve is finished (state written)
@@ -259,18 +265,22 @@ __device__ __forceinline__ float cg_dot(cg_f4 a, cg_f4 b) { return a.x * b.x + a
 // recurrence), beta_k, scipy's convergence test; the lead block records the
 // state.  Returns true when this launch has nothing to do.
 template <bool FIRST>
-__device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds, float *alpha, float *beta) {
-  __shared__ int s_exit;
+__device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds, float *alpha, float *beta,
+                                            bool *xlo_zero = nullptr) {
+  __shared__ int s_exit, s_xz;
   __shared__ float s_ab[2];
   const int tid = threadIdx.x + threadIdx.y * 64;
-  int st_done = 0;
+  int st_done = 0, st_updk = 0;
   double st_atol = 0.0, st_rho = 0.0;
   if (tid == 0) {
     st_done = g.st->done;
     st_atol = g.st->atol;
+    st_updk = g.st->upd_k;
     if (k >= 2) st_rho = g.st->rho[(k - 1) & 1];  // launch k-1's recurrence value of r.z
   }
-  double S[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  // S[5]: r.r of the residual replacement that ran between launches k-1 and
+  // k (k_cg_update), if it acted; it then replaces the recursive S[4]
+  double S[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (!FIRST) {
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
@@ -278,17 +288,25 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       for (int b = tid; b < g.nb; b += 256) s += g.part_rd[(size_t)v * PCG_MAX_BLOCKS + b];
       S[v] = wave_sum(s);
     }
+    if (g.upd_part) {
+      double s = 0.0;
+      for (int b = tid; b < g.nb; b += 256) s += g.upd_part[b];
+      S[5] = wave_sum(s);
+    }
     if ((tid & 63) == 0)
 #pragma unroll
-      for (int v = 0; v < 5; ++v) lds[v * 8 + (tid >> 6)] = S[v];
+      for (int v = 0; v < 6; ++v) lds[v * 8 + (tid >> 6)] = S[v];
   }
   __syncthreads();
   if (tid == 0) {
     int done = st_done ? -1 : 0;
     float al = 0.f, be = 0.f;
+    const bool xz = !FIRST && st_updk == k;
+    s_xz = xz;
     if (!FIRST && !done) {
 #pragma unroll
-      for (int v = 0; v < 5; ++v) S[v] = lds[v * 8] + lds[v * 8 + 1] + lds[v * 8 + 2] + lds[v * 8 + 3];
+      for (int v = 0; v < 6; ++v) S[v] = lds[v * 8] + lds[v * 8 + 1] + lds[v * 8 + 2] + lds[v * 8 + 3];
+      if (xz) S[4] = S[5];
       const double rn = sqrt(S[4]);
       const double atol = k == 1 ? g.rtol * rn : st_atol;
       if (k == 1 && S[4] == 0.0) done = 3;
@@ -334,6 +352,7 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
   __syncthreads();
   *alpha = s_ab[0];
   *beta = s_ab[1];
+  if (xlo_zero) *xlo_zero = s_xz;
   return s_exit != 0;
 }
 
@@ -538,6 +557,44 @@ __device__ __forceinline__ cg_f4 cgr_diag_raw(const CgRaw &c, cg_f4 f) {
   return cg_f4{du.x, dv.x, du.y, dv.y};
 }
 
+// b - A x at pixel (i, j) in fp64 from the fp32 operator; x + x_hi when xh
+__device__ __forceinline__ double2 resid_px(const float *__restrict__ coef, size_t ps, const float2 *__restrict__ b,
+                                           const float2 *__restrict__ x, const float2 *__restrict__ xh, int i, int j,
+                                           int H, int W, int P) {
+  const size_t k = (size_t)i * P + j;
+  auto xv = [&](size_t e) {
+    const float2 a = x[e];
+    if (!xh) return make_double2(a.x, a.y);
+    const float2 h = xh[e];
+    return make_double2((double)a.x + (double)h.x, (double)a.y + (double)h.y);
+  };
+  const double2 xc = xv(k);
+  const float2 bb = b[k];
+  double su = (double)bb.x - ((double)coef[4 * ps + k] * xc.x + (double)coef[5 * ps + k] * xc.y);
+  double sv = (double)bb.y - ((double)coef[5 * ps + k] * xc.x + (double)coef[6 * ps + k] * xc.y);
+  if (j + 1 < W) {
+    const double2 n = xv(k + 1);
+    su += (double)coef[k] * n.x;
+    sv += (double)coef[2 * ps + k] * n.y;
+  }
+  if (j > 0) {
+    const double2 n = xv(k - 1);
+    su += (double)coef[k - 1] * n.x;
+    sv += (double)coef[2 * ps + k - 1] * n.y;
+  }
+  if (i + 1 < H) {
+    const double2 n = xv(k + P);
+    su += (double)coef[ps + k] * n.x;
+    sv += (double)coef[3 * ps + k] * n.y;
+  }
+  if (i > 0) {
+    const double2 n = xv(k - P);
+    su += (double)coef[ps + k - P] * n.x;
+    sv += (double)coef[3 * ps + k - P] * n.y;
+  }
+  return make_double2(su, sv);
+}
+
 // ---------------------------------------------------------------------------
 // k_cg_small: a whole CG solve in ONE workgroup, for levels of at most
 // CG_SMALL_PX pixels.  At the coarse pyramid levels a fused k_cgs launch is
@@ -567,6 +624,8 @@ struct CgSmallArgs {
   int maxiter;
   float poly[8];
   PcgState *st;
+  float2 *xh;      // 'backslash': x_hi of the residual replacement (k_cg_update)
+  double upd_rel;  // ... done once at ||r|| < upd_rel ||b|| (0: never)
 };
 
 template <bool BLOCK>
@@ -652,8 +711,25 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
   double rr = cgs_sum(acc, lds);
   const double bnorm = sqrt(rr), atol = g.rtol * bnorm;
   double rho_prev = 1.0;
-  int it = 0, done = 0;
+  int it = 0, done = 0, upd = 0;
   for (;; ++it) {
+    if (!upd && it > 0 && sqrt(rr) < g.upd_rel * bnorm) {
+      // residual replacement (see k_cg_update): r = b - A x in fp64, x_hi = x,
+      // x_lo = 0; p and rho_prev are kept
+      acc = 0.0;
+      CGS_FOR_PIXELS(H, W) {
+        const size_t k = (size_t)i * P + j;
+        const double2 rv = resid_px(cf, ps, g.b, g.x, nullptr, i, j, H, W, P);
+        const float2 rf = make_float2((float)rv.x, (float)rv.y);
+        g.r[k] = rf;
+        g.xh[k] = g.x[k];
+        acc += (double)rf.x * rf.x + (double)rf.y * rf.y;
+      }
+      rr = cgs_sum(acc, lds);  // (barrier: every x read done)
+      CGS_FOR_PIXELS(H, W) g.x[(size_t)i * P + j] = make_float2(0.f, 0.f);
+      __syncthreads();
+      upd = 1;
+    }
     if (rr == 0.0 && it == 0) { done = 3; break; }
     if (sqrt(rr) < atol || rr == 0.0) { done = 1; break; }
     if (it >= g.maxiter) { done = 2; break; }
@@ -742,6 +818,7 @@ __global__ __launch_bounds__(CGS_BX *CGS_BY) void k_cg_small(CgSmallArgs g) {
     g.st->rr = rr;
     g.st->bnorm = bnorm;
     g.st->atol = atol;
+    g.st->upd_k = upd;
   }
 }
 template __global__ void k_cg_small<CG_DEG, true>(CgSmallArgs);
@@ -749,22 +826,21 @@ template __global__ void k_cg_small<0, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, false>(CgSmallArgs);
 
 // ---------------------------------------------------------------------------
-// k_cgs: the degree-3 iteration above with its pipeline stages split over
-// the 4 waves of a block, which all work on ONE band:
+// k_cgs: the degree-CG_DEG (5) iteration above with its pipeline stages
+// split over the 4 waves of a block, which all work on ONE band:
 //   wave 0: loads, coefficient records -> LDS ring, A) r, y of row n-1
-//   wave 1: B) g2 of row n-3, C) g1 of row n-4
-//   wave 2: D) z, p, x of row n-6, E) q, y_q of row n-7
-//   wave 3: F) v1 and the T terms of row n-9
+//   wave 1: Horner B) g4 (row n-3), g3 (n-4), g2 (n-5), g1 (n-6)
+//   wave 2: D) z, p, x of row n-8, E) q, y_q of row n-9
+//   wave 3: F) v1 and T1, T2 (row n-11), v2 and T3..T5 (row n-12)
 // with one block barrier per row step; rows cross waves through small LDS
-// rings (y, g1, y_q; records in a 12-row ring), a wave's own rows stay in
+// rings (y, g1, y_q; records in a 14-row ring), a wave's own rows stay in
 // registers.  (Round 1's k_cgp gave each wave its own band and the whole
-// pipeline: a band of R rows cost R + 12 steps of all 6 stages per wave and
-// its 32-KB record ring allowed one wave per SIMD, R = 20 at 1080p, 1.6x the
-// rows read.)  Here 64 KB of LDS per block allow 2 blocks per CU (R = 39 at
-// 1080p, 1.36x) and a step costs only the heaviest wave's share.
-// Stage lags follow from one barrier per step: a stage reads rows of another
-// wave produced at earlier steps; the band is walked for n in
-// [r0 - 5, r1 + 8] so that every row a required stage reads was produced.
+// pipeline: its record ring allowed one wave per SIMD and 1.6x the rows
+// read.)  Here 74 KB of LDS per block allow 2 blocks per CU (R = 39 at
+// 1080p) and a step costs only the heaviest wave's share.  Stage lags follow
+// from one barrier per step: a stage reads rows of another wave produced at
+// earlier steps; the band is walked for n in [r0 - 8, r1 + 11] so that every
+// row a required stage reads was produced.
 #define CGS_NREC 14
 // Load distance in row steps (each step ends at a block barrier, so a load
 // issued at step n is waited for at step n + distance): wave 0's coefficient,
@@ -903,8 +979,11 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   auto st4 = [&](float4 (&rg)[4][64], int t, cg_f4 v) { rg[t & 3][lane] = make_float4(v.x, v.y, v.z, v.w); };
   auto load_po = [&](int t) { return FIRST ? cg_f4{0.f, 0.f, 0.f, 0.f} : cg_mask1<ODD>(cg_ld4(rpo, o8(t)), ok1); };
   auto load_rin = [&](int t) { return cg_mask1<ODD>(cg_ld4(rin, o8(t)), ok1); };
+  // x_lo = 0 in the launch after a residual replacement (xz, known after
+  // the prologue; the preamble's x rows are then dropped)
+  bool xz = false;
   auto load_x = [&](int t) {
-    return (!FIRST && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
+    return (!FIRST && !xz && t >= r0 && t < r1) ? cg_mask1<ODD>(cg_ld4(rx, o8(t)), ok1) : cg_f4{0.f, 0.f, 0.f, 0.f};
   };
   const bool dm0 = out_lane && ok0, dm1 = out_lane && ok1;
   auto mdot = [&](cg_f4 a, cg_f4 b) {
@@ -948,7 +1027,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     }
   }
   float alpha = 0.f, beta = 0.f;
-  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta)) return;
+  if (cg_prologue<FIRST>(g, k, lds, &alpha, &beta, &xz)) return;
+  if (xz)
+#pragma unroll
+    for (int m = 0; m < CGS_W2N; ++m) XI[m] = zero4;
 
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (live) {
@@ -1154,6 +1236,72 @@ __global__ __launch_bounds__(256) void k_pcg_check(PcgArgs g, int k) {
   if (threadIdx.x == 0 && threadIdx.y == 0 && !g.st->done) {
     g.st->iter = k - 1;
     g.st->done = 2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Residual replacement of the 'backslash' surrogate (reliable update,
+// Sleijpen & van der Vorst 1996): the fp32 CG's recursive residual drifts
+// from b - A x by ~eps |A| |x| (|A||x| / |b| ~ 145 on Classic+NL robust
+// stages, tools/fp32_floor.py), 6x the 1e-6 target at 1080p.  Once the
+// recursive residual has fallen below upd_rel ||b|| (sqrt(rtol): 1e-3), ONE
+// launch between CG launches k-1 and k replaces it by the true residual
+// b - A x_{k-1}, evaluated in fp64 (stored fp32) from the fp32 operator, and
+// moves x_{k-1} into x_hi; launch k restarts x_lo from 0 (cg_prologue: xz)
+// and takes r.r from the replacement.  The second segment's x_lo is small,
+// so its own drift is ~1e-3 of the first's and the recursive residual then
+// tracks the true residual of x_hi + x_lo (fp64 sum) to the end; the solve's
+// result is fl32(x_hi + x_lo) (k_cg_finalize).  p, the partials and the rho
+// recurrence are kept (the replacement moves r by ~1e-5 of ||r||, far inside
+// the 10 % restart test).  Enqueued every few launches; it acts at most once
+// per solve and otherwise returns after its prologue, so the result does not
+// depend on how many were enqueued.  Grid: the solve's nb blocks, each
+// writing one r.r partial (fixed pixel set and order: deterministic).
+// Reads x (halo), b, 7 coefficient planes; writes r, x_hi: 60 B/px.
+__global__ __launch_bounds__(256) void k_cg_update(PcgArgs g, int k) {
+  __shared__ double lds[64];
+  __shared__ int s_act;
+  const int tid = threadIdx.x + threadIdx.y * 64;
+  double rr[1];
+  prologue_sum<1>(rr, g.part_rd + 4 * PCG_MAX_BLOCKS, g.nb, lds);  // launch k-1's recursive r.r
+  if (tid == 0) {
+    // every block decides alike: st->upd_k is written only with this k
+    const int updk = g.st->upd_k;
+    s_act = !g.st->done && k >= 2 && (updk == k || (updk == 0 && sqrt(rr[0]) < g.upd_rel * g.st->bnorm));
+  }
+  __syncthreads();
+  if (!s_act) return;
+  const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int H = g.H, W = g.W, P = g.P, n = H * W;
+  float2 *r = const_cast<float2 *>(g.r_in);
+  double acc[1] = {0.0};
+  for (int e = bid * 256 + tid; e < n; e += g.nb * 256) {
+    const int i = e / W, j = e - i * W;
+    const size_t kk = (size_t)i * P + j;
+    const double2 rv = resid_px(g.coef, g.ps, g.b, g.x, nullptr, i, j, H, W, P);
+    const float2 rf = make_float2((float)rv.x, (float)rv.y);
+    r[kk] = rf;
+    g.xh[kk] = g.x[kk];
+    acc[0] += (double)rf.x * rf.x + (double)rf.y * rf.y;
+  }
+  __syncthreads();  // lds reuse
+  write_partials<1>(acc, g.upd_part, lds);
+  if (tid == 0 && bid == 0) {
+    g.st->upd_k = k;
+    if (g.hflag) __hip_atomic_store(&g.hflag->upd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// the solve's result: x = fl32(x_hi + x_lo) after a residual replacement
+// (k_cg_update / k_cg_small), else x unchanged
+__global__ __launch_bounds__(256) void k_cg_finalize(float2 *x, const float2 *__restrict__ xh,
+                                                     const PcgState *st, int H, int W, int P) {
+  if (!st->upd_k) return;
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const float2 a = x[k], h = xh[k];
+    x[k] = make_float2((float)((double)a.x + (double)h.x), (float)((double)a.y + (double)h.y));
   }
 }
 
@@ -1439,39 +1587,20 @@ __global__ __launch_bounds__(256) void k_norm2_final(const double *part, int nb,
 // fp64 (A = D - N from the fp32 coefficient planes), independent of any
 // solver recurrence.  Per-block partials, then a one-block finish into
 // out[0..1].
+// fp64 true residual of x (+ x_hi when st says a residual replacement ran)
 __global__ __launch_bounds__(256) void k_resid_part(const float *__restrict__ coef, size_t ps,
                                                     const float2 *__restrict__ b, const float2 *__restrict__ x,
-                                                    int H, int W, int P, double *part) {
+                                                    const float2 *__restrict__ xh, const PcgState *st, int H, int W,
+                                                    int P, double *part) {
   __shared__ double lds[64];
   double v[2] = {0.0, 0.0};
+  const float2 *xhi = xh && st && st->upd_k ? xh : nullptr;
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
-    const float2 xc = x[k], bb = b[k];
-    double su = (double)coef[4 * ps + k] * xc.x + (double)coef[5 * ps + k] * xc.y;
-    double sv = (double)coef[5 * ps + k] * xc.x + (double)coef[6 * ps + k] * xc.y;
-    if (j + 1 < W) {
-      const float2 n = x[k + 1];
-      su -= (double)coef[k] * n.x;
-      sv -= (double)coef[2 * ps + k] * n.y;
-    }
-    if (j > 0) {
-      const float2 n = x[k - 1];
-      su -= (double)coef[k - 1] * n.x;
-      sv -= (double)coef[2 * ps + k - 1] * n.y;
-    }
-    if (i + 1 < H) {
-      const float2 n = x[k + P];
-      su -= (double)coef[ps + k] * n.x;
-      sv -= (double)coef[3 * ps + k] * n.y;
-    }
-    if (i > 0) {
-      const float2 n = x[k - P];
-      su -= (double)coef[ps + k - P] * n.x;
-      sv -= (double)coef[3 * ps + k - P] * n.y;
-    }
-    const double ru = (double)bb.x - su, rv = (double)bb.y - sv;
-    v[0] += ru * ru + rv * rv;
+    const float2 bb = b[k];
+    const double2 r = resid_px(coef, ps, b, x, xhi, i, j, H, W, P);
+    v[0] += r.x * r.x + r.y * r.y;
     v[1] += (double)bb.x * bb.x + (double)bb.y * bb.y;
   }
   write_partials<2>(v, part, lds);

@@ -6,7 +6,7 @@ share the exact struct layout.
 """
 import ctypes as C
 
-OF_ABI_VERSION = 1
+OF_ABI_VERSION = 2
 
 OF_OK, OF_EINVAL, OF_EHIP, OF_ENOMEM, OF_ENOTSUP, OF_ERCCL = 0, -1, -2, -3, -4, -5
 
@@ -81,11 +81,12 @@ class OfCgGeometry(C.Structure):
 
 class OfSolveRecord(C.Structure):
     _fields_ = [("h", C.c_int32), ("w", C.c_int32), ("solver", C.c_int32), ("iters", C.c_int32),
-                ("done", C.c_int32), ("pad_", C.c_int32), ("true_rel", C.c_double), ("est_rel", C.c_double)]
+                ("done", C.c_int32), ("pad_", C.c_int32), ("true_rel", C.c_double), ("est_rel", C.c_double),
+                ("true_rel_out", C.c_double)]
 
     def as_dict(self):
         return {"h": self.h, "w": self.w, "solver": self.solver, "iters": self.iters, "done": self.done,
-                "true_rel": self.true_rel, "est_rel": self.est_rel}
+                "true_rel": self.true_rel, "est_rel": self.est_rel, "true_rel_out": self.true_rel_out}
 
 
 def penalty(kind, p0=1.0, p1=0.0):

@@ -64,13 +64,17 @@ def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes
     if not a or len(a) != len(b):
         raise ValueError("im1s and im2s must be non-empty and of equal length")
     H, W = a[0].shape[:2]
-    if a[0].ndim == 3 and a[0].shape[2] < 3:
-        raise ValueError("estimate_flow_batch takes (H, W) or (H, W, >=3) frames")
+    # every frame of both lists: (H, W) or (H, W, >=3), checked before the
+    # [:, :, :3] slice (a 1- or 2-channel frame would otherwise pass as 3)
+    for x in a + b:
+        if not (x.ndim == 2 or (x.ndim == 3 and x.shape[2] >= 3)):
+            raise ValueError("estimate_flow_batch takes (H, W) or (H, W, >=3) frames")
     Cc = 3 if a[0].ndim == 3 else 1
+    want = (H, W, 3) if Cc == 3 else (H, W)
     a = [x[:, :, :3] if x.ndim == 3 else x for x in a]
     b = [x[:, :, :3] if x.ndim == 3 else x for x in b]
     for x in a + b:
-        if x.shape[:2] != (H, W) or (x.ndim == 3) != (Cc == 3):
+        if x.shape != want:
             raise ValueError("all frames of a batch must share one shape")
     a = [np.ascontiguousarray(x) for x in a]
     b = [np.ascontiguousarray(x) for x in b]

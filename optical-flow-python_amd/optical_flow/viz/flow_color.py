@@ -6,7 +6,6 @@ def make_colorwheel():
     segs = [(15, (255, None, 0)), (6, (None, 255, 0)), (4, (0, 255, None)),
             (11, (0, None, 255)), (13, (None, 0, 255)), (6, (255, 0, None))]
     rows = []
-    rising = {0: False, 1: True, 2: False, 3: True, 4: False, 5: True}
     for s, (n, spec) in enumerate(segs):
         ramp = np.floor(255 * np.arange(n) / n)
         block = np.zeros((n, 3))
@@ -16,7 +15,6 @@ def make_colorwheel():
             else:
                 block[:, c] = spec[c]
         rows.append(block)
-    del rising
     return np.concatenate(rows, axis=0)
 
 
@@ -40,8 +38,11 @@ def compute_color(u, v):
 
 
 def flow_to_color(flow, max_flow=None):
-    u = np.array(flow[:, :, 0], dtype=float)
-    v = np.array(flow[:, :, 1], dtype=float)
+    """(H, W, 3) uint8 Middlebury colour image; |u| or |v| > 1e9 is unknown
+    (black).  Arithmetic stays in the flow's own dtype (float32 flows are
+    coloured in float32, as the reference does)."""
+    u = np.array(flow[:, :, 0])
+    v = np.array(flow[:, :, 1])
     unknown = (np.abs(u) > 1e9) | (np.abs(v) > 1e9)
     if max_flow is not None:
         max_rad = max_flow

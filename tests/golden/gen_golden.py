@@ -374,6 +374,49 @@ def gen_altba():
     save("altba.npz", **out)
 
 
+def gen_viz_metrics():
+    """flow_to_color (viz/flow_color.py:43-107) and flow_angular_error
+    (metrics.py:5-53) on RubberWhale's ground truth (7244 unknown-flow
+    entries), the reference's own RubberWhale uv (rubberwhale_ref.npz, fp32
+    as stored and fp64), with border crops, and on a synthetic field with
+    unknown entries and flows beyond max_flow (rad > 1 saturation)."""
+    from optical_flow.viz.flow_color import flow_to_color
+    from optical_flow.evaluation.metrics import flow_angular_error
+    from optical_flow.io.flo_io import read_flo
+    gt = read_flo(os.path.join(HERE, "flow10.flo"))
+    rw = np.load(os.path.join(HERE, "rubberwhale_ref.npz"))
+    out = {}
+    out["color_gt"] = flow_to_color(gt)
+    out["color_gt_max5"] = flow_to_color(gt, max_flow=5.0)
+    rng = np.random.default_rng(77)
+    syn = rng.normal(0.0, 3.0, (37, 53, 2))
+    syn[5, 7, 0] = 1e10
+    syn[9, :, 1] = -2e9
+    syn[20:23, 30:33] = 0.0
+    out["syn"] = syn
+    out["color_syn"] = flow_to_color(syn)
+    out["color_syn_max2"] = flow_to_color(syn, max_flow=2.0)
+    out["color_syn_f32"] = flow_to_color(syn.astype(np.float32))
+    out["color_zero"] = flow_to_color(np.zeros((4, 5, 2)))
+    for name in ("classic+nl-fast", "hs-brightness"):
+        uv32 = rw[name]
+        out[f"color_{name}"] = flow_to_color(uv32)
+        out[f"color_{name}_f64"] = flow_to_color(uv32.astype(np.float64))
+        for border in (0, 10):
+            out[f"err_{name}_b{border}"] = np.array(
+                flow_angular_error(gt[..., 0], gt[..., 1], uv32[..., 0], uv32[..., 1], border))
+    # synthetic estimate against a ground truth with unknown entries (both
+    # components, and one component only), whole field and a border crop
+    est = syn + rng.normal(0.0, 0.2, syn.shape)
+    est[5, 7, 0] = 0.3
+    est[9, :, 1] = -0.1
+    out["syn_est"] = est
+    for border in (0, 3):
+        out[f"err_syn_b{border}"] = np.array(flow_angular_error(syn[..., 0], syn[..., 1], est[..., 0], est[..., 1],
+                                                                border))
+    save("viz_metrics.npz", **out)
+
+
 if __name__ == "__main__":
     jobs = sys.argv[1:] or ["unit", "e2e_small", "e2e_synth"]
     for j in jobs:

@@ -7,6 +7,7 @@ include/optflow.h declares (no compute calls without a GPU)."""
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -30,7 +31,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert set(syms) == set(_native.EXPORTED_SYMBOLS)
-    assert lib.of_abi_version() == 1
+    assert lib.of_abi_version() == 2
 
 
 def test_struct_layout_matches_header():
@@ -171,6 +172,47 @@ def test_flow_to_color():
     assert img.dtype == np.uint8 and img.shape == (20, 30, 3) and (img[0, 0] == 0).all()
 
 
+def test_flow_to_color_vs_reference(golden):
+    """flow_to_color (viz/flow_color.py:43-107) bit-exact against the
+    reference's images (tests/golden/gen_golden.py viz_metrics): RubberWhale
+    GT with 7244 unknown entries (auto and fixed max_flow), the reference's
+    own RubberWhale uv in float32 (coloured in float32) and float64, a
+    synthetic field with unknown rows/entries and rad > 1 saturation, and an
+    all-zero field."""
+    from optical_flow import flow_to_color, read_flo
+    d = golden("viz_metrics.npz")
+    gt = read_flo(os.path.join(ROOT, "tests", "golden", "flow10.flo"))
+    rw = golden("rubberwhale_ref.npz")
+    cases = {"color_gt": flow_to_color(gt), "color_gt_max5": flow_to_color(gt, max_flow=5.0),
+             "color_syn": flow_to_color(d["syn"]), "color_syn_max2": flow_to_color(d["syn"], max_flow=2.0),
+             "color_syn_f32": flow_to_color(d["syn"].astype(np.float32)),
+             "color_zero": flow_to_color(np.zeros((4, 5, 2)))}
+    for name in ("classic+nl-fast", "hs-brightness"):
+        cases[f"color_{name}"] = flow_to_color(rw[name])
+        cases[f"color_{name}_f64"] = flow_to_color(rw[name].astype(np.float64))
+    for k, img in cases.items():
+        np.testing.assert_array_equal(img, d[k], err_msg=k)
+
+
+def test_flow_angular_error_vs_reference(golden):
+    """flow_angular_error (metrics.py:5-53) against the reference on
+    RubberWhale (GT with unknown entries, borders 0 and 10) and a synthetic
+    field whose GT has unknown entries in one component only (borders 0, 3)."""
+    from optical_flow import flow_angular_error, read_flo
+    d = golden("viz_metrics.npz")
+    gt = read_flo(os.path.join(ROOT, "tests", "golden", "flow10.flo"))
+    rw = golden("rubberwhale_ref.npz")
+    for name in ("classic+nl-fast", "hs-brightness"):
+        uv = rw[name]
+        for border in (0, 10):
+            got = flow_angular_error(gt[..., 0], gt[..., 1], uv[..., 0], uv[..., 1], border)
+            np.testing.assert_allclose(got, d[f"err_{name}_b{border}"], rtol=1e-12, err_msg=f"{name} b{border}")
+    syn, est = d["syn"], d["syn_est"]
+    for border in (0, 3):
+        got = flow_angular_error(syn[..., 0], syn[..., 1], est[..., 0], est[..., 1], border)
+        np.testing.assert_allclose(got, d[f"err_syn_b{border}"], rtol=1e-12, err_msg=f"syn b{border}")
+
+
 # ---- sparse <-> planes (the narrow seam, base.py:87-114) --------------------
 def test_planes_sparse_roundtrip(golden):
     from scipy import sparse
@@ -216,3 +258,46 @@ def test_solver_geometry_bounds():
         _native.solver_geometry(64 * 257, 100, "sor")
     with pytest.raises(ValueError):
         _native.solver_geometry(0, 10, "pcg")
+
+
+def test_reference_hook_param_handling():
+    """The reference-side binding of INTEGRATION.md §3 (tools/reference_hook.py):
+    params go through parse_input_parameter ('lambda' -> lambda_, unknown keys
+    ignored, dict or flat list; base.py:65-85) before to_params()."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import reference_hook
+    from optical_flow import _abi
+    ope, P = reference_hook.params_for("classic+nl-fast", {"lambda": 3.0, "bogus_key": 1, "solver": "pcg"})
+    assert ope.lambda_ == 3.0 and P.lambda_ == 3.0 and not hasattr(ope, "bogus_key")
+    assert P.solver == _abi.SOLVER["pcg"]
+    ope, P = reference_hook.params_for("hs", ["lambda", 2.0, "max_warping_iters", 5])
+    assert P.lambda_ == 2.0 and P.max_warping_iters == 5
+    _, P0 = reference_hook.params_for("classic+nl-fast")
+    assert P0.lambda_ == load_default_lambda("classic+nl-fast")
+    with pytest.raises(ValueError):
+        reference_hook.params_for("no-such-method")
+    with pytest.raises(ValueError):
+        reference_hook.params_for("classic+nl-fast", {"solver": "lu"})
+
+
+def load_default_lambda(name):
+    from optical_flow.methods.config import load_of_method
+    return load_of_method(name).lambda_
+
+
+def test_estimate_flow_batch_rejects_mixed_channels():
+    """Every frame of both lists is checked before the [:, :, :3] slice (a 1-
+    or 2-channel frame would otherwise pass as 3 and be over-read); raised
+    before any library call."""
+    from optical_flow import estimate_flow_batch
+    rgb = np.zeros((8, 10, 3), np.uint8)
+    for bad in (np.zeros((8, 10, 2), np.uint8), np.zeros((8, 10, 1), np.uint8), np.zeros((8, 10), np.uint8),
+                np.zeros((8, 11, 3), np.uint8), np.zeros((8, 10, 3, 1), np.uint8)):
+        with pytest.raises(ValueError):
+            estimate_flow_batch([rgb, bad], [rgb, rgb])
+        with pytest.raises(ValueError):
+            estimate_flow_batch([rgb, rgb], [rgb, bad])
+    with pytest.raises(ValueError):
+        estimate_flow_batch([], [])
+    with pytest.raises(ValueError):
+        estimate_flow_batch([np.full((8, 10, 3), 300.0)], [rgb])

@@ -79,29 +79,37 @@ def test_fullsize_vs_reference(case):
         fine = [r for r in recs if r["h"] * r["w"] >= H * W // 2]
         worst = max(r["true_rel"] for r in fine)
         print(f"  {len(recs)} solves; finest-level true rel residual max {worst:.3e}; per solve "
-              + ", ".join(f"{r['h']}x{r['w']}:{r['iters']}it true {r['true_rel']:.2e} est {r['est_rel']:.2e}"
-                          for r in fine))
-        # the 'backslash' surrogate: CG to a recurrence residual of 1e-6; its
-        # true fp64 residual from the fp32 operator must stay at the fp32 floor
-        assert worst < 3e-5, worst  # measured max 8.0e-6 (GNC stage 2)
+              + ", ".join(f"{r['h']}x{r['w']}:{r['iters']}it true {r['true_rel']:.2e} est {r['est_rel']:.2e} "
+                          f"out {r['true_rel_out']:.2e}" for r in fine))
+        # the 'backslash' surrogate stops at rtol 1e-6: with its residual
+        # replacement the solver's iterate must meet that in the fp64 true
+        # residual; the returned fp32 x adds its rounding (~2e-6 floor)
+        assert worst <= 1.5e-6, worst  # measured max 9.9e-7
+        assert max(r["true_rel_out"] for r in fine) <= 3e-6  # measured max 1.44e-6
     assert abs(a_gpu - a_ref) <= 1e-3, (a_gpu, a_ref)
     assert s["mean"] <= g_mean and s["median"] <= g_med and s["p99"] <= g_p99, s
 
 
 def test_fullsize_1080_default_solve_log():
     """Config 4 with the default solver: every solve's true fp64 residual
-    (of_solve_log) at the fp32 floor, and the AEPE against the analytic GT
-    within 1e-3 of the reference's pcg run (the reference's 'backslash' run at
-    1080p is the ref1080_backslash fixture when it exists; see above)."""
+    (of_solve_log) within 1.5x the surrogate's rtol (1e-6) for the solver's
+    iterate, within 3x for the returned fp32 x (rounding a solution of these
+    systems to fp32 alone leaves ~2e-6 on robust stages: |A||x|/|b| ~ 145,
+    tools/fp32_floor.py), and the AEPE against the analytic GT within 1e-3 of
+    the reference's pcg run (the reference's own 'backslash' run at 1080p is
+    the ref1080_backslash fixture above)."""
     d = dict(np.load(os.path.join(GOLDEN, "ref1080_pcg_sub4.npz")))
     uv, gt, recs = _run("classic+nl-fast", None, 1080, 1920, log=True)
     assert np.all(np.isfinite(uv))
     assert len(recs) == 27, len(recs)  # 7 levels x 3 + 2 GNC levels x 3 (SURVEY.md §8)
     for r in recs:
-        print(f"  {r['h']}x{r['w']} iters {r['iters']} done {r['done']} true {r['true_rel']:.3e} est {r['est_rel']:.3e}")
+        print(f"  {r['h']}x{r['w']} iters {r['iters']} done {r['done']} true {r['true_rel']:.3e} est {r['est_rel']:.3e} "
+              f"out {r['true_rel_out']:.3e}")
     assert all(r["done"] in (1, 3) for r in recs), [r for r in recs if r["done"] not in (1, 3)]
     worst = max(r["true_rel"] for r in recs)
-    assert worst < 3e-5, worst  # measured max 8.0e-6 (GNC stage 2)
+    assert worst <= 1.5e-6, worst  # measured max 9.9e-7 (the est agrees to 4 digits)
+    assert all(abs(r["true_rel"] - r["est_rel"]) <= 0.05 * r["true_rel"] for r in recs)
+    assert max(r["true_rel_out"] for r in recs) <= 3e-6  # measured max 1.44e-6
     a_gpu = _aepe(uv, gt)
     print(f"AEPE gpu backslash {a_gpu:.6f}  ref pcg {float(d['aepe_gt']):.6f}")
-    assert abs(a_gpu - float(d["aepe_gt"])) <= 2e-3
+    assert abs(a_gpu - float(d["aepe_gt"])) <= 1e-3  # measured 1.2e-5

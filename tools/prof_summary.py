@@ -64,6 +64,7 @@ def main():
     write, wmeta = load_counters(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
     hit, hmeta = load_counters(os.path.join(d, "l2_counter_collection.csv"), "TCC_HIT_sum")
     miss, _ = load_counters(os.path.join(d, "l2_counter_collection.csv"), "TCC_MISS_sum")
+    valu, vmeta = load_counters(os.path.join(d, "valu_counter_collection.csv"), "SQ_INSTS_VALU")
 
     def per_key(vals, meta):
         acc = collections.defaultdict(list)
@@ -72,6 +73,7 @@ def main():
         return acc
 
     F, Wr, Hh, M = per_key(fetch, fmeta), per_key(write, wmeta), per_key(hit, hmeta), per_key(miss, hmeta)
+    V = per_key(valu, vmeta)
     # finest-level dispatches: the grid with the most pixels per kernel name
     rows = []
     names = {}
@@ -101,6 +103,9 @@ def main():
         if wk:
             wk = sorted(wk)[len(wk) // 2:]
             rec["write_MB"] = round(sum(wk) / len(wk) * 1024 / 1e6, 3)
+        vk = V.get((n, g), [])
+        if vk:  # VALU wave-instructions per finest-level dispatch (median)
+            rec["valu_insts_per_launch"] = int(sorted(vk)[len(vk) // 2])
         hk, mk = Hh.get((n, g), []), M.get((n, g), [])
         if hk and mk and sum(hk) + sum(mk) > 0:
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
@@ -134,6 +139,7 @@ def main():
                                      "fetch_MB": r.get("fetch_MB"),
                                      "write_MB": r.get("write_MB"), "grid": r["finest_grid"],
                                      "l2_hit": r.get("l2_hit"),
+                                     "valu_insts_per_launch": r.get("valu_insts_per_launch"),
                                      "note": "2*FETCH_SIZE + WRITE_SIZE (KB->B) per dispatch at the finest level "
                                              "(FETCH_SIZE x2: gfx950 tallies 128-B requests at 64 B); "
                                              "Infinity-Cache (MALL) hits are included in FETCH_SIZE"}

@@ -4,6 +4,8 @@
 #      and of bench.py --lanes 1 (the isolated durations the bench roofline uses)
 #   2-4. PMC FETCH_SIZE / WRITE_SIZE / TCC hit+miss, each in its own pass
 #        (MI355X_MICROARCH.md rocprofv3 section), on one serial 1080p pair
+#   5. PMC SQ_INSTS_VALU / SQ_WAVES of the weighted median (its VALU-issue
+#      roofline in the bench line)
 # usage: tools/profile.sh TAG
 set -u
 TAG=$1; shift
@@ -18,3 +20,4 @@ tools/gpu_step.sh 400 $OUT/trace1.log rocprofv3 --kernel-trace --stats -f csv -d
 tools/gpu_step.sh 300 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $S || exit $?
 tools/gpu_step.sh 300 $OUT/write.log rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o write -- python3 $S || exit $?
 tools/gpu_step.sh 300 $OUT/l2.log rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT -o l2 -- python3 $S || exit $?
+tools/gpu_step.sh 300 $OUT/valu.log rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-include-regex 'k_wmf' -f csv -d $OUT -o valu -- python3 $S || exit $?
