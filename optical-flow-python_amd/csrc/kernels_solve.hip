@@ -563,7 +563,7 @@ __device__ __forceinline__ double2 resid_px(const float *__restrict__ coef, size
                                            int H, int W, int P) {
   const size_t k = (size_t)i * P + j;
   auto xv = [&](size_t e) {
-    const float2 a = x[e];
+    const float2 a = x ? x[e] : make_float2(0.f, 0.f);
     if (!xh) return make_double2(a.x, a.y);
     const float2 h = xh[e];
     return make_double2((double)a.x + (double)h.x, (double)a.y + (double)h.y);
@@ -1292,15 +1292,22 @@ __global__ __launch_bounds__(256) void k_cg_update(PcgArgs g, int k) {
   }
 }
 
+// x_lo is part of the iterate only if a CG launch after the replacement ran
+// its sweep: a solve that the replacement itself finished (its residual
+// already below atol, declared by launch upd_k, iter = upd_k - 1) never
+// restarted x_lo, which then still holds x_hi's copy
+__device__ __forceinline__ bool cg_xlo_live(const PcgState *st) { return st->iter >= st->upd_k; }
+
 // the solve's result: x = fl32(x_hi + x_lo) after a residual replacement
 // (k_cg_update / k_cg_small), else x unchanged
 __global__ __launch_bounds__(256) void k_cg_finalize(float2 *x, const float2 *__restrict__ xh,
                                                      const PcgState *st, int H, int W, int P) {
   if (!st->upd_k) return;
+  const bool lo = cg_xlo_live(st);
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
-    const float2 a = x[k], h = xh[k];
+    const float2 a = lo ? x[k] : make_float2(0.f, 0.f), h = xh[k];
     x[k] = make_float2((float)((double)a.x + (double)h.x), (float)((double)a.y + (double)h.y));
   }
 }
@@ -1595,11 +1602,12 @@ __global__ __launch_bounds__(256) void k_resid_part(const float *__restrict__ co
   __shared__ double lds[64];
   double v[2] = {0.0, 0.0};
   const float2 *xhi = xh && st && st->upd_k ? xh : nullptr;
+  const float2 *xlo = xhi && !cg_xlo_live(st) ? nullptr : x;
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     const float2 bb = b[k];
-    const double2 r = resid_px(coef, ps, b, x, xhi, i, j, H, W, P);
+    const double2 r = resid_px(coef, ps, b, xlo, xhi, i, j, H, W, P);
     v[0] += r.x * r.x + r.y * r.y;
     v[1] += (double)bb.x * bb.x + (double)bb.y * bb.y;
   }

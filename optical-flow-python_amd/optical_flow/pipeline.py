@@ -9,9 +9,9 @@ from ONE `of_pairs_run_host` call (`estimate_flow_batch`: `lanes` pairs in
 flight, H2D/D2H overlapped inside the library), and the host file work is
 overlapped with the GPU:
 
-    decode pool   : chunk j+1's PNGs (+ GT .flo)     \
+    decode pool   : chunk j+1's PNGs (+ GT .flo)                  \
     this thread   : chunk j on the GPU (ctypes releases the GIL)   } at once
-    writer thread : chunk j-1's .flo files + AAE/AEPE               /
+    writer pool   : chunk j-1's .flo files + AAE/AEPE              /
 
 Pairs are grouped by frame shape (Middlebury sequences differ in size) and
 results come back in job order.  Each flow equals `estimate_flow(im1, im2,
@@ -87,20 +87,20 @@ def _finish(job, uv, gt, border):
     return res
 
 
-def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=3, chunk=8, workers=4, border=0,
+def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=3, chunk=8, workers=4, writers=2, border=0,
                  keep_flows=False, flow_fn=None):
     """Run `jobs` (PairJob list) through decode -> flow -> write + metrics
     with the three stages overlapped.  Returns (results, stats): one dict
     per job in job order ({name, shape, out, [aae, std_ae, aepe], [uv]}) and
     wall-clock stats {pairs, wall_s, pairs_per_s, decode_s, gpu_s, write_s}
-    (decode_s / write_s are busy times summed over their threads, so overlap
-    shows as gpu_s ~ wall_s).  `flow_fn(im1s, im2s)` replaces the GPU batch
+    (decode_s / write_s are busy times summed over their `workers` /
+    `writers` threads, so overlap shows as gpu_s ~ wall_s).  `flow_fn(im1s, im2s)` replaces the GPU batch
     call (host-logic tests); by default estimate_flow_batch(..., method,
     params, lanes)."""
     if not jobs:
         return [], {"pairs": 0, "wall_s": 0.0, "pairs_per_s": 0.0, "decode_s": 0.0, "gpu_s": 0.0, "write_s": 0.0}
-    if chunk < 1 or workers < 1:
-        raise ValueError("chunk and workers must be >= 1")
+    if chunk < 1 or workers < 1 or writers < 1:
+        raise ValueError("chunk, workers and writers must be >= 1")
     if flow_fn is None:
         from optical_flow.interface import estimate_flow_batch
 
@@ -119,7 +119,7 @@ def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=3, chunk=8, 
             with lock:
                 busy[key] += time.perf_counter() - t0
 
-    with ThreadPoolExecutor(workers) as dec, ThreadPoolExecutor(1) as wr:
+    with ThreadPoolExecutor(workers) as dec, ThreadPoolExecutor(writers) as wr:
         # decode runs ahead of the GPU by up to 2 chunks (bounded host
         # memory); chunks are consecutive decoded pairs of one shape, at most
         # `chunk` long (shapes are known only after decoding)

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--lanes", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=8)
+    ap.add_argument("--workers", type=int, default=6)
+    ap.add_argument("--writers", type=int, default=3)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     tmp = a.out or tempfile.mkdtemp(prefix="ofpipe_")
@@ -45,16 +47,19 @@ def main():
         f2.append(im2.astype(np.uint8))
         jobs.append(PairJob(f"p{k:03d}", os.path.join(d, "frame10.png"), os.path.join(d, "frame11.png"),
                             os.path.join(d, "gt.flo"), os.path.join(d, "out.flo")))
+        if k % 8 == 7:
+            print(f"wrote {k + 1} pairs", flush=True)
     estimate_flow_batch(f1[:a.lanes], f2[:a.lanes], lanes=a.lanes)  # warm-up: arenas, lanes, code objects
     t0 = time.perf_counter()
     for s in range(0, a.pairs, a.chunk):
         estimate_flow_batch(f1[s:s + a.chunk], f2[s:s + a.chunk], lanes=a.lanes)
     mem = a.pairs / (time.perf_counter() - t0)
-    res, st = run_pipeline(jobs, lanes=a.lanes, chunk=a.chunk)
+    res, st = run_pipeline(jobs, lanes=a.lanes, chunk=a.chunk, workers=a.workers, writers=a.writers)
     aepe = float(np.mean([r["aepe"] for r in res]))
     print(json.dumps({"metric": "file-to-file pairs/s (PNG decode -> flow -> .flo + AAE/AEPE)",
                       "value": round(st["pairs_per_s"], 3), "in_memory_pairs_per_s": round(mem, 3),
                       "pairs": a.pairs, "height": a.height, "width": a.width, "lanes": a.lanes, "chunk": a.chunk,
+                      "workers": a.workers, "writers": a.writers,
                       "wall_s": round(st["wall_s"], 3), "gpu_busy_s": round(st["gpu_s"], 3),
                       "decode_busy_s": round(st["decode_s"], 3), "write_busy_s": round(st["write_s"], 3),
                       "mean_aepe_gt": round(aepe, 5)}), flush=True)
