@@ -688,6 +688,11 @@ void cheb_poly(int m, double a, double b, double *cB) {
 #ifndef CGS_TARGET_BLOCKS
 #define CGS_TARGET_BLOCKS PCG_MAX_BLOCKS
 #endif
+// fewest rows per k_cgs band (coarse levels, where the band count is not
+// capped by CGS_TARGET_BLOCKS): a launch walks R + 19 row steps
+#ifndef CGS_MIN_R
+#define CGS_MIN_R 8
+#endif
 int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
   if (H < 1 || W < 1) return OF_EINVAL;
   const int sw = split ? PCG_SWP : PCG_SW;
@@ -695,7 +700,7 @@ int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
   if (nstrips > PCG_MAX_BLOCKS) return OF_ENOTSUP;
   int nbands, R, gy;
   if (split) {
-    nbands = std::max(1, std::min((H + 7) / 8, CGS_TARGET_BLOCKS / nstrips));
+    nbands = std::max(1, std::min((H + CGS_MIN_R - 1) / CGS_MIN_R, CGS_TARGET_BLOCKS / nstrips));
     R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
     gy = nbands;
@@ -1021,13 +1026,15 @@ struct LevelIn {
   Img guide;  // gc planes or p == nullptr
 };
 
-// Lanes mode (of_pairs_run, of_pairs_run_host): a linear solve on a level of
-// >= big_px pixels (solve_tok below; nothing else takes the token) holds the
-// lanes' shared token until its GPU work has drained, so at most one pair at a
-// time streams a fine CG working set (1080p: ~190 MB, most of the 256 MB
-// Infinity Cache) and two lanes' 512-block CG launches never interleave.
-// Preprocessing, warps, assembly and the weighted median of fine levels run
-// unserialised.  Outside lanes mode: no-op.
+// Lanes mode (of_pairs_run, of_pairs_run_host): the full-size preprocessing
+// (ROF, pyramids) and every linear solve on a level of >= big_px pixels
+// (solve_tok below) hold the lanes' shared token until their GPU work has
+// drained, so at most one pair at a time streams a fine CG working set
+// (1080p: ~190 MB, most of the 256 MB Infinity Cache) and two lanes' 512-block
+// CG launches never interleave.  Warps, assembly and the weighted median of
+// fine levels run unserialised.  Tried and rejected (round 3): the token
+// holder's solve on a shared high-priority stream, 32.3-32.8 vs 35.5-36.2
+// pairs/s (profiles/r3f_cg_priority_ab.log).  Outside lanes mode: no-op.
 struct BigPhase {
   of_ctx *c;
   bool held = false;

@@ -334,6 +334,24 @@ def gen_full480sor():
     _full("ref480_hs_sor_sub2.npz", 480, 640, "hs", {"solver": "sor"}, 2)
 
 
+def gen_chaos720():
+    """Config 3's sensitivity in the reference itself: classic-c / pcg on
+    synth_pair(720, 1280, 0) with frame 1 perturbed by 1e-12 relative noise
+    (seeded), vs the unperturbed ref720_classic_c_pcg_sub4.npz: EPE statistics
+    on the same 4x subsampled grid.  Calibrates the fp32-vs-f64 gate of
+    tests/test_gpu_fullsize.py (charbonnier GNC is chaotic).  ~8 min."""
+    im1, im2, gt = synthetic.synth_pair(720, 1280, 0)
+    rng = np.random.default_rng(720)
+    im1p = im1 * (1.0 + 1e-12 * rng.standard_normal(im1.shape))
+    uv = quiet(ref.estimate_flow, im1p, im2, "classic-c", {"solver": "pcg"})
+    base = np.load(os.path.join(HERE, "ref720_classic_c_pcg_sub4.npz"))["uv_sub4"].astype(np.float64)
+    e = np.sqrt(((uv[::4, ::4] - base) ** 2).sum(-1))
+    st = {"mean": float(e.mean()), "median": float(np.median(e)), "p99": float(np.percentile(e, 99)),
+          "max": float(e.max()), "aepe_gt": _aepe(uv, gt)}
+    print("  chaos720:", st)
+    save("chaos720.npz", **{k: np.array(v) for k, v in st.items()})
+
+
 def gen_altba():
     """AltBA (classic-c-a) parity vectors.  The registry's classic-c-a
     diverges in the reference (|uv| ~ 3.6e36 on the crop); lambda2 = 0.01

@@ -56,7 +56,11 @@ def main():
     a = ap.parse_args()
     import bench  # noqa: E402  (KERNEL_BYTES_PER_PX, profiler names)
     d = a.dir
-    trace = list(csv.DictReader(open(os.path.join(d, "trace_kernel_trace.csv"))))
+    # durations from the isolated (lanes = 1) trace when present: a kernel's
+    # own duration, not stretched by another lane's kernels (bench roofline)
+    tname = "trace1_kernel_trace.csv" if os.path.exists(os.path.join(d, "trace1_kernel_trace.csv")) else \
+        "trace_kernel_trace.csv"
+    trace = list(csv.DictReader(open(os.path.join(d, tname))))
     dur = collections.defaultdict(list)
     for r in trace:
         dur[(short(r["Kernel_Name"]), grid_key(r))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
