@@ -38,8 +38,11 @@ def _aepe(uv, gt):
 CASES = {
     "cfg2_hs_sor_480": ("ref480_hs_sor_sub2.npz", 480, 640, "hs", {"solver": "sor"}, 2,
                         (1e-3, 5e-5, 1e-2)),  # measured 2.0e-4 / 4.7e-6 / 2.2e-3
+    # charbonnier GNC is chaotic: the reference itself moves by 8.1e-3 / 5.8e-3 /
+    # 4.1e-2 under a 1e-12 perturbation of frame 1 (chaos720.npz); measured
+    # GPU 9.1e-3 / 6.6e-3 / 4.2e-2, gated at ~2x the reference's own spread
     "cfg3_classic_c_pcg_720": ("ref720_classic_c_pcg_sub4.npz", 720, 1280, "classic-c", {"solver": "pcg"}, 4,
-                               (3e-2, 2e-2, 0.15)),  # measured 9.4e-3 / 6.7e-3 / 4.6e-2 (charbonnier: chaotic)
+                               (1.6e-2, 1.2e-2, 8e-2)),
     "cfg4_classic_nl_fast_pcg_1080": ("ref1080_pcg_sub4.npz", 1080, 1920, "classic+nl-fast", {"solver": "pcg"}, 4,
                                       (1e-3, 2e-4, 1e-2)),  # measured 2.3e-4 / 4.6e-5 / 2.9e-3
     "cfg4_classic_nl_fast_1080": ("ref1080_backslash_sub4.npz", 1080, 1920, "classic+nl-fast", None, 4,
@@ -88,6 +91,11 @@ def test_fullsize_vs_reference(case):
         assert max(r["true_rel_out"] for r in fine) <= 3e-6  # measured max 1.44e-6
     assert abs(a_gpu - a_ref) <= 1e-3, (a_gpu, a_ref)
     assert s["mean"] <= g_mean and s["median"] <= g_med and s["p99"] <= g_p99, s
+    if case.startswith("cfg3"):
+        ch = dict(np.load(os.path.join(GOLDEN, "chaos720.npz")))
+        print(f"  reference's own spread under a 1e-12 perturbation: mean {float(ch['mean']):.2e} "
+              f"median {float(ch['median']):.2e} p99 {float(ch['p99']):.2e}")
+        assert s["mean"] <= 2 * float(ch["mean"]) and s["median"] <= 2 * float(ch["median"])
 
 
 def test_fullsize_1080_default_solve_log():
