@@ -830,7 +830,6 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     a.rtol = rtol;
     a.maxiter = block ? P->exact_maxiter : P->pcg_maxiter;
     a.xh = xh.p;
-    a.upd_part = block ? c->d_partials + 15 * PCG_MAX_BLOCKS : nullptr;
     a.upd_rel = upd_rel;
     HIPCHK(hipMemsetAsync(c->d_state, 0, sizeof(PcgState), c->stream));
     auto args_k = [&](int k) {

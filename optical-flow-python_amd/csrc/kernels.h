@@ -61,5 +61,9 @@ struct PcgState {
   // the k_cg_update that acted (0: none yet).  That launch starts x_lo from
   // 0 and takes r.r from the update; x = x_hi + x_lo from then on.
   int upd_k;
+  // launch whose prologue first saw ||r|| < upd_rel ||b|| (0: not yet): the
+  // replacement offered after it acts
+  int upd_due;
+  int pad_;
   double xnorm2, dnorm2;  // SOR
 };

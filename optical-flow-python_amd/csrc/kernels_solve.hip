@@ -98,10 +98,9 @@ struct PcgArgs {
   int maxiter;
   float poly[8];  // k_cgs: M^-1 = (poly[0] + poly[1] B + ... + poly[CG_DEG] B^CG_DEG) D^-1
   // 'backslash' residual replacement (k_cg_update; null / 0 for 'pcg'):
-  // x_hi (the iterate at the replacement), the replacement's per-block r.r
-  // partials, and the relative residual at which it acts
+  // x_hi (the iterate at the replacement) and the relative residual at which
+  // it acts
   float2 *xh;
-  double *upd_part;
   double upd_rel;
 };
 
@@ -278,9 +277,10 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
     st_updk = g.st->upd_k;
     if (k >= 2) st_rho = g.st->rho[(k - 1) & 1];  // launch k-1's recurrence value of r.z
   }
-  // S[5]: r.r of the residual replacement that ran between launches k-1 and
-  // k (k_cg_update), if it acted; it then replaces the recursive S[4]
-  double S[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  // after a residual replacement (k_cg_update between launches k-1 and k)
+  // S[4] is already the replaced residual's r.r: the update wrote it into
+  // launch k-1's partials
+  double S[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (!FIRST) {
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
@@ -288,14 +288,9 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
       for (int b = tid; b < g.nb; b += 256) s += g.part_rd[(size_t)v * PCG_MAX_BLOCKS + b];
       S[v] = wave_sum(s);
     }
-    if (g.upd_part) {
-      double s = 0.0;
-      for (int b = tid; b < g.nb; b += 256) s += g.upd_part[b];
-      S[5] = wave_sum(s);
-    }
     if ((tid & 63) == 0)
 #pragma unroll
-      for (int v = 0; v < 6; ++v) lds[v * 8 + (tid >> 6)] = S[v];
+      for (int v = 0; v < 5; ++v) lds[v * 8 + (tid >> 6)] = S[v];
   }
   __syncthreads();
   if (tid == 0) {
@@ -305,8 +300,7 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
     s_xz = xz;
     if (!FIRST && !done) {
 #pragma unroll
-      for (int v = 0; v < 6; ++v) S[v] = lds[v * 8] + lds[v * 8 + 1] + lds[v * 8 + 2] + lds[v * 8 + 3];
-      if (xz) S[4] = S[5];
+      for (int v = 0; v < 5; ++v) S[v] = lds[v * 8] + lds[v * 8 + 1] + lds[v * 8 + 2] + lds[v * 8 + 3];
       const double rn = sqrt(S[4]);
       const double atol = k == 1 ? g.rtol * rn : st_atol;
       if (k == 1 && S[4] == 0.0) done = 3;
@@ -330,6 +324,9 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
         g.st->rr = S[4];
         g.st->rho[k & 1] = rho;
         if (done) g.st->done = done;
+        // residual replacement due (k_cg_update): read by update launches only
+        if (!done && g.upd_rel > 0.0 && k >= 2 && rn < g.upd_rel * g.st->bnorm && !g.st->upd_due)
+          g.st->upd_due = k;
       }
       al = (float)a_;
       be = drift ? 0.f : (float)(rho / S[3]);
@@ -1262,12 +1259,12 @@ __global__ __launch_bounds__(256) void k_cg_update(PcgArgs g, int k) {
   __shared__ double lds[64];
   __shared__ int s_act;
   const int tid = threadIdx.x + threadIdx.y * 64;
-  double rr[1];
-  prologue_sum<1>(rr, g.part_rd + 4 * PCG_MAX_BLOCKS, g.nb, lds);  // launch k-1's recursive r.r
   if (tid == 0) {
-    // every block decides alike: st->upd_k is written only with this k
+    // every block decides alike: upd_due was set by an earlier CG launch's
+    // prologue (its recursive residual below upd_rel ||b||), and st->upd_k
+    // is written only with this k
     const int updk = g.st->upd_k;
-    s_act = !g.st->done && k >= 2 && (updk == k || (updk == 0 && sqrt(rr[0]) < g.upd_rel * g.st->bnorm));
+    s_act = !g.st->done && k >= 2 && (updk == k || (updk == 0 && g.st->upd_due > 0));
   }
   __syncthreads();
   if (!s_act) return;
@@ -1284,8 +1281,10 @@ __global__ __launch_bounds__(256) void k_cg_update(PcgArgs g, int k) {
     g.xh[kk] = g.x[kk];
     acc[0] += (double)rf.x * rf.x + (double)rf.y * rf.y;
   }
-  __syncthreads();  // lds reuse
-  write_partials<1>(acc, g.upd_part, lds);
+  // the replaced r.r into launch k-1's partial slot 4, which launch k's
+  // prologue sums (each block writes only its own slot; no block of this
+  // launch reads the partials)
+  write_partials<1>(acc, const_cast<double *>(g.part_rd) + 4 * PCG_MAX_BLOCKS, lds);
   if (tid == 0 && bid == 0) {
     g.st->upd_k = k;
     if (g.hflag) __hip_atomic_store(&g.hflag->upd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1350,8 +1349,12 @@ __global__ __launch_bounds__(256) void k_cg_finalize(float2 *x, const float2 *__
 //   - the stopping test of sweep k-1 runs in the prologue of launch k on the
 //     per-strip fp64 partials (fixed order, so every block agrees), ping-
 //     ponged by sweep parity.
-#define SOR_D 4    // prefetch distance in steps
+#ifndef SOR_D
+#define SOR_D 4    // prefetch distance in steps (<= 7: ring of 8)
+#endif
+#ifndef SOR_G
 #define SOR_G 64   // steps between progress publications
+#endif
 #define SOR_MAXS (PCG_MAX_BLOCKS / 2)
 
 struct SorArgs {
