@@ -1349,11 +1349,14 @@ __global__ __launch_bounds__(256) void k_cg_finalize(float2 *x, const float2 *__
 //   - the stopping test of sweep k-1 runs in the prologue of launch k on the
 //     per-strip fp64 partials (fixed order, so every block agrees), ping-
 //     ponged by sweep parity.
+// prefetch distance in steps (<= 7: ring of 8) and steps between progress
+// publications: 7 / 32 vs 4 / 64 = 0.94 vs 1.15 ms per 480x640 sweep, the
+// same iterate (profiles/r3i_sor_ab.log; 16 / 8 steps: 0.89 / 0.91 ms)
 #ifndef SOR_D
-#define SOR_D 4    // prefetch distance in steps (<= 7: ring of 8)
+#define SOR_D 7
 #endif
 #ifndef SOR_G
-#define SOR_G 64   // steps between progress publications
+#define SOR_G 32
 #endif
 #define SOR_MAXS (PCG_MAX_BLOCKS / 2)
 

@@ -205,8 +205,12 @@ def test_altba_compute_flow_base(golden, alpha, rep):
     is 3.6e6 (vs 4.0e3 at alpha = 1, measured with scipy eigsh), so merely
     rounding the assembled float64 system to float32 and solving it exactly
     moves the increment by 1.5e-3 px mean (measured); the fp32 GPU path is
-    at 7.6e-3 mean / 5.2e-3 median after 4 warps, which the alpha = 0 bound
-    states."""
+    at 7.8e-3 mean / 7.3e-3 median after 4 warps, which the alpha = 0 bound
+    states.  Its 'backslash' solves meet rtol 1e-6 in the true residual, but
+    at condition 3.6e6 a 1e-6 residual still leaves up to ~3.6 x the
+    solution's scale of error; a tighter rtol is out of reach of fp32 CG on
+    this system (round 3: rtol 1e-8 stalls at a 0.17 relative residual after
+    20000 iterations of the first warp's solve)."""
     from optical_flow.methods.config import load_of_method
     d = golden("altba.npz")
     o = load_of_method("classic-c-a")
@@ -220,40 +224,6 @@ def test_altba_compute_flow_base(golden, alpha, rep):
     mean_tol, med_tol = (5e-4, 5e-5) if alpha == 1.0 else (2e-2, 1e-2)
     _uv_close(uv, d[key + "_uv"], mean_tol, med_tol)
     _uv_close(uvhat, d[key + "_uvhat"], mean_tol, med_tol)
-
-
-@pytest.mark.parametrize("rep", [True, False])
-def test_altba_alpha0_tight_rtol(golden, rep):
-    """Where the alpha = 0 gap above comes from: the 'backslash' surrogate
-    meets rtol 1e-6 in the true residual (solve log), but on a system with
-    condition number 3.6e6 a 1e-6 residual leaves an error of up to ~3.6 x
-    the solution's scale, so the x it returns differs from the reference's
-    exact solve.  With rtol 1e-8 the same GPU path must come down toward the
-    fp32 floor of this case (1.5e-3 px mean: rounding the assembled float64
-    system to float32 and solving it exactly, measured with scipy)."""
-    from optical_flow import _native
-    from optical_flow.methods.config import load_of_method
-    d = golden("altba.npz")
-    o = load_of_method("classic-c-a")
-    o.images = d["base_images"]
-    o.lambda2 = 0.01
-    o.max_iters = 4
-    o.alpha = 0.0
-    o.replacement = rep
-    o.backslash_rtol = 1e-8
-    o.backslash_maxiter = 20000
-    ctx = _native.context()
-    ctx.set_solve_log(True)
-    try:
-        uv, uvhat = o.compute_flow_base(d["base_uv"], d["base_uvhat"])
-        recs = ctx.solve_log()
-    finally:
-        ctx.set_solve_log(False)
-    print(f"{len(recs)} solves, iters {[r['iters'] for r in recs]}, true rel max {max(r['true_rel'] for r in recs):.2e}")
-    assert all(r["done"] == 1 and r["true_rel"] <= 1.5e-8 for r in recs), recs
-    key = f"base_a0_r{int(rep)}"
-    _uv_close(uv, d[key + "_uv"], 4e-3, 4e-3)
-    _uv_close(uvhat, d[key + "_uvhat"], 4e-3, 4e-3)
 
 
 @pytest.mark.parametrize("tag,sz,lam,it", [("5_0.3_1", [5, 5], 0.3, 1), ("5_0.7_3", [5, 5], 0.7, 3),
