@@ -803,8 +803,12 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
       a.st = c->d_state;
       a.xh = xh.p;
       a.upd_rel = upd_rel;
-      launch(c, "pcg_small", block ? k_cg_small<CG_DEG, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY), 0,
-             a);
+      if ((double)H * W <= CG_REG_PX)
+        launch(c, "pcg_small", block ? k_cg_reg<CG_DEG, true> : k_cg_reg<0, false>, dim3(1), dim3(64, CGR_T / 64), 0,
+               a);
+      else
+        launch(c, "pcg_small", block ? k_cg_small<CG_DEG, true> : k_cg_small<0, false>, dim3(1), dim3(CGS_BX, CGS_BY),
+               0, a);
       if (block) finish_backslash(c, coef, b, x, xh);
       HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
       return res;

@@ -823,6 +823,223 @@ template __global__ void k_cg_small<0, true>(CgSmallArgs);
 template __global__ void k_cg_small<0, false>(CgSmallArgs);
 
 // ---------------------------------------------------------------------------
+// k_cg_reg: the same whole-solve-in-one-workgroup CG (scipy control flow,
+// same preconditioners, the 'backslash' residual replacement) for levels of
+// at most CG_REG_PX = 2048 pixels (17x30 and 34x60 at 1080p), with every
+// vector in REGISTERS: thread t owns the pixels e = t + 512 m (m < CGR_M) of
+// the dense row-major index e = i W + j, holds their coefficients, D^-1 and
+// x, r, p, y, g, q, and exchanges neighbour values through a double-buffered
+// LDS copy of the one field a stencil application reads (one barrier per
+// exchange: 6 per iteration at degree 5), and reduces dot products through
+// per-wave LDS slots in a fixed order (one barrier each; deterministic).
+// k_cg_small walked every vector through global memory with a barrier per
+// sweep: ~14 us per iteration at 17x30 / 34x60.
+// 512 threads (2 waves per SIMD: up to 256 VGPRs) x 4 pixels; 1024 x 4
+// spilled 656 B/lane at the 128 VGPRs a 1024-thread block allows, 1024 x 2
+// still 100 B/lane
+#define CGR_T 512
+#define CGR_M 4
+#define CG_REG_PX (CGR_T * CGR_M)
+
+template <int DEG, bool BLOCK>
+__global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
+  __shared__ float2 ex[2][CG_REG_PX];
+  __shared__ double red[2][CGR_T / 64][2];
+  const int tid = threadIdx.x + threadIdx.y * CGS_BX, wv = tid >> 6;
+  const int H = g.H, W = g.W, P = g.P, N = H * W;
+  const size_t ps = g.ps;
+  const float *cf = g.coef;
+  int e[CGR_M], ir[CGR_M], jr[CGR_M];
+  bool ok[CGR_M];
+  size_t kk[CGR_M];
+  // coefficients: weights of the edges right / left / down / up (u, v),
+  // the 2x2 block (a, c, d) and its inverse (ia, ic, id)
+  float wr_u[CGR_M], wl_u[CGR_M], wd_u[CGR_M], wu_u[CGR_M], wr_v[CGR_M], wl_v[CGR_M], wd_v[CGR_M], wu_v[CGR_M];
+  float ca[CGR_M], cc[CGR_M], cd[CGR_M], ia[CGR_M], ic[CGR_M], id[CGR_M];
+  float2 x[CGR_M], r[CGR_M], p[CGR_M];
+#pragma unroll
+  for (int m = 0; m < CGR_M; ++m) {
+    e[m] = tid + CGR_T * m;
+    ok[m] = e[m] < N;
+    const int ee = ok[m] ? e[m] : 0;
+    ir[m] = ee / W;
+    jr[m] = ee - ir[m] * W;
+    kk[m] = (size_t)ir[m] * P + jr[m];
+    const size_t k = kk[m];
+    const int i = ir[m], j = jr[m];
+    wr_u[m] = ok[m] && j + 1 < W ? cf[k] : 0.f;
+    wl_u[m] = ok[m] && j > 0 ? cf[k - 1] : 0.f;
+    wd_u[m] = ok[m] && i + 1 < H ? cf[ps + k] : 0.f;
+    wu_u[m] = ok[m] && i > 0 ? cf[ps + k - P] : 0.f;
+    wr_v[m] = ok[m] && j + 1 < W ? cf[2 * ps + k] : 0.f;
+    wl_v[m] = ok[m] && j > 0 ? cf[2 * ps + k - 1] : 0.f;
+    wd_v[m] = ok[m] && i + 1 < H ? cf[3 * ps + k] : 0.f;
+    wu_v[m] = ok[m] && i > 0 ? cf[3 * ps + k - P] : 0.f;
+    ca[m] = ok[m] ? cf[4 * ps + k] : 0.f;
+    cc[m] = ok[m] ? cf[5 * ps + k] : 0.f;
+    cd[m] = ok[m] ? cf[6 * ps + k] : 0.f;
+    if (ok[m]) {
+      cgs_inv<BLOCK>(cf, ps, k, ia[m], ic[m], id[m]);
+    } else {
+      ia[m] = ic[m] = id[m] = 0.f;
+    }
+    x[m] = make_float2(0.f, 0.f);
+    r[m] = ok[m] ? g.b[k] : make_float2(0.f, 0.f);
+    p[m] = make_float2(0.f, 0.f);
+  }
+  int buf = 0, rb = 0;
+  // neighbour sum N f of owned pixel m after exch(f)
+  // (macro, not a lambda taking the array: an array reference kept the
+  // Horner temporaries addressable and spilled them to scratch)
+#define CGR_EXCH(f)                                  \
+  {                                                   \
+    _Pragma("unroll") for (int m = 0; m < CGR_M; ++m) \
+      if (ok[m]) ex[buf][e[m]] = (f)[m];              \
+    __syncthreads();                                  \
+  }
+  auto nsum = [&](int m) {
+    const float2 *X = ex[buf];
+    const int c = ok[m] ? e[m] : 0;
+    const float2 L = X[max(c - 1, 0)], R = X[min(c + 1, N - 1)], U = X[max(c - W, 0)], D = X[min(c + W, N - 1)];
+    return make_float2(wl_u[m] * L.x + wr_u[m] * R.x + wu_u[m] * U.x + wd_u[m] * D.x,
+                       wl_v[m] * L.y + wr_v[m] * R.y + wu_v[m] * U.y + wd_v[m] * D.y);
+  };
+  auto minv = [&](int m, float2 f) { return make_float2(ia[m] * f.x + ic[m] * f.y, ic[m] * f.x + id[m] * f.y); };
+  // fixed-order fp64 sums of two per-thread values over the workgroup
+  auto reduce2 = [&](double v0, double v1, double &s0, double &s1) {
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    if ((tid & 63) == 0) {
+      red[rb][wv][0] = v0;
+      red[rb][wv][1] = v1;
+    }
+    __syncthreads();
+    s0 = 0.0;
+    s1 = 0.0;
+#pragma unroll
+    for (int w = 0; w < CGR_T / 64; ++w) {
+      s0 += red[rb][w][0];
+      s1 += red[rb][w][1];
+    }
+    rb ^= 1;
+  };
+  double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+  for (int m = 0; m < CGR_M; ++m) acc0 += (double)(r[m].x * r[m].x + r[m].y * r[m].y);
+  double rr, dummy;
+  reduce2(acc0, 0.0, rr, dummy);
+  const double bnorm = sqrt(rr), atol = g.rtol * bnorm;
+  double rho_prev = 1.0;
+  int it = 0, done = 0, upd = 0;
+  for (;; ++it) {
+    if (!upd && it > 0 && sqrt(rr) < g.upd_rel * bnorm) {
+      // residual replacement (see k_cg_update): r = b - A x in fp64, x_hi = x,
+      // x_lo = 0; p and rho_prev are kept
+      CGR_EXCH(x);
+      acc0 = 0.0;
+#pragma unroll
+      for (int m = 0; m < CGR_M; ++m) {
+        const float2 *X = ex[buf];
+        const int c = ok[m] ? e[m] : 0;
+        const float2 L = X[max(c - 1, 0)], R = X[min(c + 1, N - 1)], U = X[max(c - W, 0)], D = X[min(c + W, N - 1)];
+        const float2 bm = ok[m] ? g.b[kk[m]] : make_float2(0.f, 0.f);
+        const double su = (double)bm.x - ((double)ca[m] * x[m].x + (double)cc[m] * x[m].y) +
+                          (double)wl_u[m] * L.x + (double)wr_u[m] * R.x + (double)wu_u[m] * U.x +
+                          (double)wd_u[m] * D.x;
+        const double sv = (double)bm.y - ((double)cc[m] * x[m].x + (double)cd[m] * x[m].y) +
+                          (double)wl_v[m] * L.y + (double)wr_v[m] * R.y + (double)wu_v[m] * U.y +
+                          (double)wd_v[m] * D.y;
+        r[m] = ok[m] ? make_float2((float)su, (float)sv) : make_float2(0.f, 0.f);
+        acc0 += (double)r[m].x * r[m].x + (double)r[m].y * r[m].y;
+        if (ok[m]) g.xh[kk[m]] = x[m];  // x_hi (read back by k_cg_finalize)
+        x[m] = make_float2(0.f, 0.f);
+      }
+      buf ^= 1;
+      reduce2(acc0, 0.0, rr, dummy);
+      upd = 1;
+    }
+    if (rr == 0.0 && it == 0) { done = 3; break; }
+    if (sqrt(rr) < atol || rr == 0.0) { done = 1; break; }
+    if (it >= g.maxiter) { done = 2; break; }
+    // z = M^-1 r (Horner in B = D^-1 N), rho = r.z
+    float2 z[CGR_M];
+    if (DEG == 0) {
+#pragma unroll
+      for (int m = 0; m < CGR_M; ++m) z[m] = minv(m, r[m]);
+    } else {
+      float2 y[CGR_M];
+#pragma unroll
+      for (int m = 0; m < CGR_M; ++m) y[m] = minv(m, r[m]);
+      CGR_EXCH(y);
+#pragma unroll
+      for (int m = 0; m < CGR_M; ++m) {
+        const float2 ny = minv(m, nsum(m));
+        z[m] = make_float2(g.poly[DEG - 1] * y[m].x + g.poly[DEG] * ny.x, g.poly[DEG - 1] * y[m].y + g.poly[DEG] * ny.y);
+      }
+      buf ^= 1;
+#pragma unroll
+      for (int d = DEG - 2; d >= 0; --d) {
+        CGR_EXCH(z);
+#pragma unroll
+        for (int m = 0; m < CGR_M; ++m) {
+          const float2 ng = minv(m, nsum(m));
+          z[m] = make_float2(g.poly[d] * y[m].x + ng.x, g.poly[d] * y[m].y + ng.y);
+        }
+        buf ^= 1;
+      }
+    }
+    acc0 = 0.0;
+#pragma unroll
+    for (int m = 0; m < CGR_M; ++m) acc0 += (double)(r[m].x * z[m].x + r[m].y * z[m].y);
+    double rho;
+    reduce2(acc0, 0.0, rho, dummy);
+    const float beta = it == 0 ? 0.f : (float)(rho / rho_prev);
+#pragma unroll
+    for (int m = 0; m < CGR_M; ++m) p[m] = make_float2(z[m].x + beta * p[m].x, z[m].y + beta * p[m].y);
+    // q = A p = D p - N p, pq = p.q
+    CGR_EXCH(p);
+    float2 q[CGR_M];
+    acc0 = 0.0;
+#pragma unroll
+    for (int m = 0; m < CGR_M; ++m) {
+      const float2 np = nsum(m);
+      q[m] = make_float2(ca[m] * p[m].x + cc[m] * p[m].y - np.x, cc[m] * p[m].x + cd[m] * p[m].y - np.y);
+      acc0 += (double)(p[m].x * q[m].x + p[m].y * q[m].y);
+    }
+    buf ^= 1;
+    double pq;
+    reduce2(acc0, 0.0, pq, dummy);
+    if (!(pq > 0.0) || !(rho > 0.0)) { done = 1; break; }  // underflow (see cg_prologue)
+    const float alpha = (float)(rho / pq);
+    acc0 = 0.0;
+#pragma unroll
+    for (int m = 0; m < CGR_M; ++m) {
+      x[m] = make_float2(x[m].x + alpha * p[m].x, x[m].y + alpha * p[m].y);
+      r[m] = make_float2(r[m].x - alpha * q[m].x, r[m].y - alpha * q[m].y);
+      acc0 += (double)(r[m].x * r[m].x + r[m].y * r[m].y);
+    }
+    reduce2(acc0, 0.0, rr, dummy);
+    rho_prev = rho;
+  }
+#pragma unroll
+  for (int m = 0; m < CGR_M; ++m)
+    if (ok[m]) {
+      g.x[kk[m]] = x[m];
+    }
+  if (tid == 0) {
+    g.st->iter = it;
+    g.st->done = done;
+    g.st->rr = rr;
+    g.st->bnorm = bnorm;
+    g.st->atol = atol;
+    g.st->upd_k = upd;
+  }
+#undef CGR_EXCH
+}
+template __global__ void k_cg_reg<CG_DEG, true>(CgSmallArgs);
+template __global__ void k_cg_reg<0, false>(CgSmallArgs);
+
+// ---------------------------------------------------------------------------
 // k_cgs: the degree-CG_DEG (5) iteration above with its pipeline stages
 // split over the 4 waves of a block, which all work on ONE band:
 //   wave 0: loads, coefficient records -> LDS ring, A) r, y of row n-1
