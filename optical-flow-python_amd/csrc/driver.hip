@@ -866,7 +866,9 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
                                   : (odd ? k_cg<false, false, true> : k_cg<false, false, false>));
       launch(c, "pcg_iter", kern, grid, blk, 0, args_k(k), k, R, nbands);
     });
-    launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
+    // the convergence test of the last enqueued iterate when the solve ran
+    // out of launches (a no-op, skipped, once a prologue declared it done)
+    if (!hf->done) launch(c, "pcg_check", k_pcg_check, dim3(1), blk, 0, args_k(enq), enq);
     if (block) finish_backslash(c, coef, b, x, xh);
     HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     return res;
@@ -997,7 +999,10 @@ void median2(of_ctx *c, const F2 &in, const F2 &out, int size) {
     throw OfError{OF_ENOTSUP, "median_filter_size must be 3, 5 or 7"};
 }
 
-void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &out, int hsz, double sigma_i) {
+// out = weighted median of uv; with base: out = base + (median - base)
+// (classic_nl.py:271-275's uv0 + (filtered - uv0), fused; out may be base)
+void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &out, int hsz, double sigma_i,
+         const float2 *base = nullptr) {
   REQUIRE(guide.C == 1 || guide.C == 3, OF_ENOTSUP, "weighted median guide must have 1 or 3 channels");
   REQUIRE(hsz >= 0 && hsz <= 12, OF_ENOTSUP, "area_hsz must be <= 12");
   const int RW = WMF_T + 2 * hsz, nreg = RW * RW;
@@ -1012,7 +1017,7 @@ void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &
   auto pick = [&](auto k1, auto k2, auto k4, auto k8, auto k8h7, auto k16) {
     auto k = nper == 1 ? k1 : nper == 2 ? k2 : nper == 4 ? k4 : nper == 8 ? (hsz == 7 ? k8h7 : k8) : k16;
     launch(c, "wmf", k, grid, dim3(64), shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H, uv.W,
-           uv.P, guide.ps(), hsz, nk, RW, RP);
+           uv.P, guide.ps(), hsz, nk, RW, RP, base);
   };
   if (guide.C == 3)
     pick(k_wmf<3, 1, 0>, k_wmf<3, 2, 0>, k_wmf<3, 4, 0>, k_wmf<3, 8, 0>, k_wmf<3, 8, 7>, k_wmf<3, 16, 0>);
@@ -1120,13 +1125,20 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
              (const float2 *)uv.p, (const float2 *)x.p, P->limit_update, uv1.p, (const float *)L.im.p,
              (const float *)L.im.plane(nc), nc, (nl && filt && L.guide.p) ? occ.p : (float *)nullptr, H, W, uv.P,
              L.im.ps());
+      const bool last = jl + 1 >= max_linear;
+      if (last && filt && nl && L.guide.p) {
+        // uv = uv0 + (filtered - uv0) (classic_nl.py:271-275) in the weighted
+        // median's own store
+        wmf(c, uv1, L.guide, occ.p, uv, P->area_hsz, P->sigma_i, (const float2 *)uv.p);
+        continue;
+      }
       F2 res = uv1;
       if (filt) {
         if (nl && L.guide.p) wmf(c, uv1, L.guide, occ.p, uv2, P->area_hsz, P->sigma_i);
         else median2(c, uv1, uv2, P->median_filter_size);
         res = uv2;
       }
-      if (jl + 1 < max_linear)  // duv = filtered - uv feeds the next linearisation
+      if (!last)  // duv = filtered - uv feeds the next linearisation
         launch(c, "sub2", k_sub2, g.grid, g.block, 0, (const float2 *)uv.p, (const float2 *)res.p, duv.p, H, W, uv.P);
       else  // uv = uv0 + (filtered - uv0)  (classic_nl.py:271-275, ba.py:404-407)
         launch(c, "axpy_diff", k_axpy_diff, g.grid, g.block, 0, uv.p, (const float2 *)uv.p, (const float2 *)res.p, H,

@@ -529,8 +529,9 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
 // scheduler use the registers to keep LDS reads in flight
 template <int GC, int NPER, int HS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_wmf(const float2 *__restrict__ uv, const float *__restrict__ guide,
-                                             const float *__restrict__ occ, float2 *__restrict__ out, int H, int W,
-                                             int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt) {
+                                             const float *__restrict__ occ, float2 *out, int H, int W,
+                                             int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt,
+                                             const float2 *base) {
   using T = typename WmfRec<GC>::T;
   constexpr int N = NPER * 64, CH = N / WMF_NC;
   const int hsz = HS > 0 ? HS : hsz_rt;
@@ -697,12 +698,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     // the selected samples' values, re-read at their (mirrored) positions
     const int ya = mir(ty0 - hsz + (int)(resu >> 8), H), xa = mir(tx0 - hsz + (int)(resu & 0xffu), W);
     const int yb = mir(ty0 - hsz + (int)(resv >> 8), H), xb = mir(tx0 - hsz + (int)(resv & 0xffu), W);
-    out[(size_t)gi * P + gj] = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
+    float2 med = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
+    if (base) {  // out = base + (med - base): classic_nl.py:271-275 fused (out may alias base)
+      const float2 b0 = base[(size_t)gi * P + gj];
+      med = make_float2(b0.x + (med.x - b0.x), b0.y + (med.y - b0.y));
+    }
+    out[(size_t)gi * P + gj] = med;
   }
 }
 #define OF_WMF(GC, NP, HS)                                                                                       \
   template __global__ void k_wmf<GC, NP, HS>(const float2 *, const float *, const float *, float2 *, int, int, int, \
-                                              size_t, int, float, int, int);
+                                              size_t, int, float, int, int, const float2 *);
 OF_WMF(1, 1, 0) OF_WMF(1, 2, 0) OF_WMF(1, 4, 0) OF_WMF(1, 8, 0) OF_WMF(1, 16, 0) OF_WMF(1, 8, 7)
 OF_WMF(3, 1, 0) OF_WMF(3, 2, 0) OF_WMF(3, 4, 0) OF_WMF(3, 8, 0) OF_WMF(3, 16, 0) OF_WMF(3, 8, 7)
 #undef OF_WMF
