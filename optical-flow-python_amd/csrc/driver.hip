@@ -676,6 +676,12 @@ void cheb_poly(int m, double a, double b, double *cB) {
 // but moves the 48x64 smoke pair's mean |uv - oracle| from 6.7e-4 to 6.1e-3
 // (knob sweep).
 #define CG_CHEB_A 0.04
+// the robust GNC stages (alpha < 0.5: D^-1 A with more small eigenvalues):
+// 0.02 takes 479 instead of 488 CG iterations per 1080p pair (+1.5 %
+// pairs/s; profiles/r3q_cheb_robust_ab.log)
+#ifndef CG_CHEB_A_ROBUST
+#define CG_CHEB_A_ROBUST 0.02
+#endif
 
 // Launch geometry of the fused CG iteration kernels for an H x W level.
 // k_cg ('pcg'): strips of PCG_SW columns x bands of R rows, 4 bands (waves)
@@ -763,7 +769,7 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     float poly[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (block) {
       double cb[CG_DEG + 1];
-      cheb_poly(CG_DEG, CG_CHEB_A, 2.0, cb);
+      cheb_poly(CG_DEG, P->alpha < 0.5 ? CG_CHEB_A_ROBUST : CG_CHEB_A, 2.0, cb);
       for (int i = 0; i <= CG_DEG; ++i) poly[i] = (float)cb[i];
     }
     // ring slot of this solve; a slot is reused only after a synchronisation
