@@ -547,6 +547,72 @@ __device__ __forceinline__ cg_f4 cgr_diag(const CgRec &m, cg_f4 f) {
   }
   return cg_cat(o[0], o[1]);
 }
+// Pair-block splitting of k_cgs's preconditioner (CGS_PAIR): the lane's two
+// pixels (columns 2k, 2k+1 of the image, the same pairs in every tile) form
+// one 4x4 block D' = [[D0, -W], [-W, D1]] of A = D' - N', W = diag(wu, wv)
+// the weights of the edge inside the pair, N' = N without that edge.  The
+// Chebyshev polynomial is taken in B' = D'^-1 N' instead of D^-1 N, for the
+// same LDS record size: the record keeps D0^-1 in ma/mb[0] and S1^-1 =
+// (D1 - W D0^-1 W)^-1 (the Schur complement) in ma/mb[1].  Offline
+// (tools/pair_block_iters.py) it needed 0.75x the robust-stage iterations,
+// but those operators carry a row-only flow perturbation that makes the
+// horizontal edges dominate.  On the GPU (round 3, profiles/r3t_*): 479 ->
+// 449 CG iterations per 1080p pair, 48.8 -> 52.2 us per active 1080p launch
+// (the block elimination lengthens every stage's dependency chain), 38.29 vs
+// 38.42 pairs/s.  Off by default; kept as an A/B switch.
+#ifndef CGS_PAIR
+#define CGS_PAIR 0
+#endif
+// N' f (N f without the edge inside the pair)
+__device__ __forceinline__ cg_f4 cgr_nsum_p(cg_f4 up, cg_f4 mid, cg_f4 dn, const CgRec &c, const cg_f2 (&wu)[2]) {
+#if CGS_PAIR
+  const cg_f2 m0 = cg_lo(mid), m1 = cg_hi(mid);
+  const cg_f2 L = cg_left2(m1), Rt = cg_right2(m0), wl = cg_left2(c.wx[1]);
+  const cg_f2 s0 = wl * L + wu[0] * cg_lo(up) + c.wy[0] * cg_lo(dn);
+  const cg_f2 s1 = c.wx[1] * Rt + wu[1] * cg_hi(up) + c.wy[1] * cg_hi(dn);
+  return cg_cat(s0, s1);
+#else
+  return cgr_nsum(up, mid, dn, c, wu);
+#endif
+}
+// D'^-1 f by block elimination: y0' = D0^-1 f0, y1 = S1^-1 (f1 + W y0'),
+// y0 = y0' + D0^-1 W y1
+__device__ __forceinline__ cg_f4 cgr_pinv(const CgRec &m, cg_f4 r) {
+#if CGS_PAIR
+  const cg_f2 y0 = m.ma[0] * r.x + m.mb[0] * r.y;
+  const cg_f2 t = cg_hi(r) + m.wx[0] * y0;
+  const cg_f2 y1 = m.ma[1] * t.x + m.mb[1] * t.y;
+  const cg_f2 s = m.wx[0] * y1;
+  return cg_cat(y0 + (m.ma[0] * s.x + m.mb[0] * s.y), y1);
+#else
+  return cgr_minv(m, r);
+#endif
+}
+// D f (the 2x2 blocks of A) from a record: D0 re-formed from D0^-1, D1 =
+// S1 + W D0^-1 W with S1 re-formed from S1^-1
+__device__ __forceinline__ cg_f4 cgr_diag_p(const CgRec &m, cg_f4 f) {
+#if CGS_PAIR
+  cg_f2 o[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float ia = m.ma[e].x, ic = m.ma[e].y, id = m.mb[e].y;
+    const float det = ia * id - ic * ic;
+    const float inv = det != 0.f ? __builtin_amdgcn_rcpf(det) : 0.f;
+    cg_f2 da = cg_f2{id, -ic} * inv, db = cg_f2{-ic, ia} * inv;
+    if (e == 1) {
+      const float wu = m.wx[0].x, wv = m.wx[0].y, ia0 = m.ma[0].x, ic0 = m.ma[0].y, id0 = m.mb[0].y;
+      const float cuv = wu * wv * ic0;
+      da += cg_f2{wu * wu * ia0, cuv};
+      db += cg_f2{cuv, wv * wv * id0};
+    }
+    const float fu = e ? f.z : f.x, fv = e ? f.w : f.y;
+    o[e] = da * fu + db * fv;
+  }
+  return cg_cat(o[0], o[1]);
+#else
+  return cgr_diag(m, f);
+#endif
+}
 // D f from the raw coefficient row (wave 0 still holds it): no inverse
 __device__ __forceinline__ cg_f4 cgr_diag_raw(const CgRaw &c, cg_f4 f) {
   const cg_f2 u = cg_f2{f.x, f.z}, v = cg_f2{f.y, f.w};
@@ -1159,6 +1225,17 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     cc.a = c.a;
     cc.c = c.c;
     cc.d = c.d;
+#if CGS_PAIR
+    // pixel 1's entry becomes the Schur complement S1 = D1 - W D0^-1 W
+    {
+      CgCoef c0 = cc;
+      const CgInv m0 = cg_inv<true>(c0);
+      const float wu = c.wxu.x, wv = c.wxv.x;
+      cc.a.y = c.a.y - wu * wu * m0.ia.x;
+      cc.c.y = c.c.y - wu * wv * m0.ic.x;
+      cc.d.y = c.d.y - wv * wv * m0.id.x;
+    }
+#endif
     const CgInv mi = cg_inv<true>(cc);
     float4 *q = &ring[rslot(t)][0][lane];
     q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
@@ -1293,7 +1370,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         get_wy(n - 2, wu);
         cg_f4 r = RI[RRI(-1)];
         if (!FIRST) r -= alpha * (cgr_diag_raw(SG[RSG(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
-        const cg_f4 y = cgr_minv(q1, r);
+        const cg_f4 y = cgr_pinv(q1, r);
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
         if (o >= r0 && o < r1) {
@@ -1317,29 +1394,29 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 4, wu);
           const cg_f4 y0 = yrow(n - 3);
-          const cg_f4 ny = cgr_nsum(yrow(n - 4), y0, yrow(n - 2), q, wu);
-          G4[R4(-3)] = c4 * y0 + c5 * cgr_minv(q, ny);
+          const cg_f4 ny = cgr_nsum_p(yrow(n - 4), y0, yrow(n - 2), q, wu);
+          G4[R4(-3)] = c4 * y0 + c5 * cgr_pinv(q, ny);
         }
         {
           const CgRec q = get_rec(n - 4);
           cg_f2 wu[2];
           get_wy(n - 5, wu);
-          const cg_f4 ng = cgr_nsum(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
-          G3[R4(-4)] = c3 * yrow(n - 4) + cgr_minv(q, ng);
+          const cg_f4 ng = cgr_nsum_p(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
+          G3[R4(-4)] = c3 * yrow(n - 4) + cgr_pinv(q, ng);
         }
         {
           const CgRec q = get_rec(n - 5);
           cg_f2 wu[2];
           get_wy(n - 6, wu);
-          const cg_f4 ng = cgr_nsum(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
-          G2[R4(-5)] = c2 * yrow(n - 5) + cgr_minv(q, ng);
+          const cg_f4 ng = cgr_nsum_p(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
+          G2[R4(-5)] = c2 * yrow(n - 5) + cgr_pinv(q, ng);
         }
         {
           const CgRec q = get_rec(n - 6);
           cg_f2 wu[2];
           get_wy(n - 7, wu);
-          const cg_f4 ng = cgr_nsum(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, wu);
-          st4(s_g1, n - 6, c1 * yrow(n - 6) + cgr_minv(q, ng));
+          const cg_f4 ng = cgr_nsum_p(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, wu);
+          st4(s_g1, n - 6, c1 * yrow(n - 6) + cgr_pinv(q, ng));
         }
       })
     } else if (role == 2) {
@@ -1352,10 +1429,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           const CgRec q4 = get_rec(n - 8);
           cg_f2 wu[2];
           get_wy(n - 9, wu);
-          const cg_f4 ng = cgr_nsum(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
+          const cg_f4 ng = cgr_nsum_p(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
           const float4 b = s_y[(n - 8) & 7][lane];
           const cg_f4 yr = {b.x, b.y, b.z, b.w};
-          const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
+          const cg_f4 z = c0 * yr + cgr_pinv(q4, ng);
           cg_f4 p = FIRST ? z : z + beta * PO2[RW2(-8)];
           const int o = n - 8;
           const bool rv = (unsigned)o < (unsigned)H;
@@ -1376,8 +1453,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 10, wu);
           const cg_f4 pm = PP[R4(-9)];
-          const cg_f4 q = cgr_diag(q5, pm) - cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
-          const cg_f4 yq = cgr_minv(q5, q);
+          const cg_f4 q = cgr_diag_p(q5, pm) - cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
+          const cg_f4 yq = cgr_pinv(q5, q);
           st4(s_yq, n - 9, yq);
           const int o = n - 9;
           if (o >= r0 && o < r1) {
@@ -1399,8 +1476,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 12, wu);
           const cg_f4 yq = ld4(s_yq, n - 11);
-          const cg_f4 ny = cgr_nsum(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
-          const cg_f4 v1 = cgr_minv(q6, ny);
+          const cg_f4 ny = cgr_nsum_p(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
+          const cg_f4 v1 = cgr_pinv(q6, ny);
           V1[R4(-11)] = v1;
           const int o = n - 11;
           if (o >= r0 && o < r1) {
@@ -1413,15 +1490,20 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wy7[2];
           get_wy(n - 13, wy7);
           const cg_f4 v1 = V1[R4(-12)];
-          const cg_f4 nv = cgr_nsum(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
-          const cg_f4 v2 = cgr_minv(q7, nv);
+          const cg_f4 nv = cgr_nsum_p(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
+          const cg_f4 v2 = cgr_pinv(q7, nv);
           const cg_f4 vu = V2[R2(-13)];
           V2[R2(-12)] = v2;
           const int o = n - 12;
           if (o >= r0 && o < r1) {
             const cg_f2 w0 = cg_lo(v2), w1 = cg_hi(v2);
             const cg_f2 h0 = cg_left2(q7.wx[1]) * cg_left2(w1) + wy7[0] * cg_lo(vu);
+#if CGS_PAIR
+            (void)w0;  // N' has no edge inside the pair
+            const cg_f2 h1 = wy7[1] * cg_hi(vu);
+#else
             const cg_f2 h1 = q7.wx[0] * w0 + wy7[1] * cg_hi(vu);
+#endif
             const cg_f4 t = (c3 * v1 + c4 * v2) * nv + (2.0f * c5) * v2 * cg_cat(h0, h1);
             acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
           }
