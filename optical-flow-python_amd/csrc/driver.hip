@@ -1044,15 +1044,20 @@ struct LevelIn {
   Img guide;  // gc planes or p == nullptr
 };
 
-// Lanes mode (of_pairs_run, of_pairs_run_host): the full-size preprocessing
-// (ROF, pyramids) and every linear solve on a level of >= big_px pixels
-// (solve_tok below) hold the lanes' shared token until their GPU work has
-// drained, so at most one pair at a time streams a fine CG working set
+// Lanes mode (of_pairs_run, of_pairs_run_host): every linear solve on a
+// level of >= big_px pixels (solve_tok below) holds the lanes' shared token
+// until its GPU work has drained, so at most one pair at a time streams a fine CG working set
 // (1080p: ~190 MB, most of the 256 MB Infinity Cache) and two lanes' 512-block
 // CG launches never interleave.  Warps, assembly and the weighted median of
 // fine levels run unserialised.  Tried and rejected (round 3): the token
 // holder's solve on a shared high-priority stream, 32.3-32.8 vs 35.5-36.2
 // pairs/s (profiles/r3f_cg_priority_ab.log).  Outside lanes mode: no-op.
+// The full-size preprocessing (ROF, pyramids) ran under the token through
+// round 3; without it (A/B, 2 x 2 reps): 39.02 vs 38.40 pairs/s host to
+// host, bitwise the same flows (profiles/r3u_ab.log, r3v_ab.log)
+#ifndef OF_PRE_TOKEN
+#define OF_PRE_TOKEN 0
+#endif
 struct BigPhase {
   of_ctx *c;
   bool held = false;
@@ -1227,8 +1232,8 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
   REQUIRE(nc >= 1 && nc <= OF_MAX_NC, OF_ENOTSUP, "1..4 channels per frame supported");
   hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
   HIPCHK(hipEventRecord(t0, c->stream));
-  // preprocessing
-  std::unique_ptr<BigPhase> pre(new BigPhase(c, (double)H * W));
+  // preprocessing (under the lanes' token with OF_PRE_TOKEN)
+  std::unique_ptr<BigPhase> pre(new BigPhase(c, OF_PRE_TOKEN ? (double)H * W : 0.0));
   Img img;
   if (P->texture) {
     const double alp = (P->method == OF_METHOD_HS || P->method == OF_METHOD_ALT_BA) ? 0.95 : P->alp;

@@ -1132,6 +1132,15 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #ifndef CGS_PF2
 #define CGS_PF2 1
 #endif
+// no loads past the last row the band's outputs depend on (the drain steps
+// of the walk; ~7 % of a band's reads).  Bitwise the same; as OOB offsets
+// 38.29 vs 38.40 pairs/s (no gain: the row step is not load-bound), and a
+// first version that skipped the loads and stage A by branches ran at 26.3
+// (the branches forced every outstanding load to be waited for)
+// (profiles/r3u_ab.log, r3v_ab.log).  Off by default.
+#ifndef CGS_TRIM
+#define CGS_TRIM 0
+#endif
 #define CGS_POW2(n) ((n) <= 1 ? 1 : (n) <= 2 ? 2 : (n) <= 4 ? 4 : 8)
 #define CGS_SGN CGS_POW2(CGS_PF + 2)
 #define CGS_RIN CGS_POW2(CGS_PF + 1)
@@ -1203,10 +1212,15 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   const int r0 = flip ? H - rb1 : rb0, r1 = flip ? H - rb0 : rb1;
   const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3], c4 = g.poly[4], c5 = g.poly[5];
   auto orow = [&](int t) { return (unsigned)(flip ? H - 1 - t : t); };
-  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? orow(t) * rowb4 : CG_ROW_OOB); };
-  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? orow(t) * rowb8 : CG_ROW_OOB); };
+  // rows past vlim feed no output of the band (stage A is needed up to row
+  // r1 + 7, p_old up to r1 + 8): their loads take the out-of-range offset,
+  // which reads 0 without touching memory (CGS_TRIM; branch-free, so the
+  // load pipelining is unchanged)
+  const int vlim = CGS_TRIM ? min(H, r1 + 9) : H;
+  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)vlim ? orow(t) * rowb4 : CG_ROW_OOB); };
+  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)vlim ? orow(t) * rowb8 : CG_ROW_OOB); };
   auto o4w = [&](int t) {
-    return flip ? off4 + ((unsigned)t < (unsigned)(H - 1) ? (unsigned)(H - 2 - t) * rowb4 : CG_ROW_OOB) : o4(t);
+    return flip ? off4 + ((unsigned)t < (unsigned)min(H - 1, vlim) ? (unsigned)(H - 2 - t) * rowb4 : CG_ROW_OOB) : o4(t);
   };
   auto load_raw = [&](int t, CgRaw &c) {
     const unsigned v = o4(t), vw = o4w(t);

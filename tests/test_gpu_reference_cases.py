@@ -205,8 +205,8 @@ def test_altba_compute_flow_base(golden, alpha, rep):
     is 3.6e6 (vs 4.0e3 at alpha = 1, measured with scipy eigsh), so merely
     rounding the assembled float64 system to float32 and solving it exactly
     moves the increment by 1.5e-3 px mean (measured); the fp32 GPU path is
-    at 7.8e-3 mean / 7.3e-3 median after 4 warps, which the alpha = 0 bound
-    states.  Its 'backslash' solves meet rtol 1e-6 in the true residual, but
+    at 7.5e-3 mean / 7.2e-3 median after 4 warps (1.06e-2 / 9.8e-3 without
+    the replacement step), which the alpha = 0 bounds state.  Its 'backslash' solves meet rtol 1e-6 in the true residual, but
     at condition 3.6e6 a 1e-6 residual still leaves up to ~3.6 x the
     solution's scale of error; a tighter rtol is out of reach of fp32 CG on
     this system (round 3: rtol 1e-8 stalls at a 0.17 relative residual after
@@ -221,7 +221,9 @@ def test_altba_compute_flow_base(golden, alpha, rep):
     o.replacement = rep
     uv, uvhat = o.compute_flow_base(d["base_uv"], d["base_uvhat"])
     key = f"base_a{int(alpha)}_r{int(rep)}"
-    mean_tol, med_tol = (5e-4, 5e-5) if alpha == 1.0 else (2e-2, 1e-2)
+    # alpha = 0 measured (round 3, honest-residual solver): replacement 7.5e-3 /
+    # 7.2e-3, no replacement 1.06e-2 / 9.8e-3 px mean / median (deterministic)
+    mean_tol, med_tol = (5e-4, 5e-5) if alpha == 1.0 else (1.6e-2, 1.2e-2)
     _uv_close(uv, d[key + "_uv"], mean_tol, med_tol)
     _uv_close(uvhat, d[key + "_uvhat"], mean_tol, med_tol)
 
