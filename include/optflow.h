@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OF_ABI_VERSION 2
+#define OF_ABI_VERSION 3
 
 /* status codes */
 #define OF_OK 0
@@ -65,6 +65,25 @@ typedef struct of_penalty {
   double p0;   /* sigma, or r for t-dist */
   double p1;   /* a for generalized charbonnier, s for t-dist */
 } of_penalty;
+
+/*
+ * A general spatial_filters list (classic_nl.py:301-322, ba.py:228-246,
+ * alt_ba.py:298-316): filter i is fh[i] x fw[i] taps (row-major, at most
+ * 5 x 5), applied as the reference's make_convn_mat(F, sz, 'valid',
+ * 'sameswap') (utils/sparse_ops.py:59-109) with its own penalties.  general
+ * = 0 means the default pair [[1, -1]], [[1], [-1]] with rho_spatial_* /
+ * qua_spatial_* of of_params (the matrix-free 5-point hot path).
+ */
+#define OF_MAX_FILTERS 8
+#define OF_MAX_FDIM 5
+typedef struct of_filter_set {
+  int32_t general;
+  int32_t n;
+  int32_t fh[OF_MAX_FILTERS], fw[OF_MAX_FILTERS];
+  double taps[OF_MAX_FILTERS][OF_MAX_FDIM * OF_MAX_FDIM];
+  of_penalty rho_u[OF_MAX_FILTERS], rho_v[OF_MAX_FILTERS];
+  of_penalty qua_u[OF_MAX_FILTERS], qua_v[OF_MAX_FILTERS];
+} of_filter_set;
 
 /*
  * POD mirror of the method object's attribute bag
@@ -114,6 +133,7 @@ typedef struct of_params {
   of_penalty rho_data, rho_spatial_u[2], rho_spatial_v[2];
   of_penalty qua_data, qua_spatial_u[2], qua_spatial_v[2];  /* quadratic relaxation */
   of_penalty rho_couple;        /* AltBA */
+  of_filter_set filters;        /* ABI 3: general spatial_filters */
 } of_params;
 
 /* per-call statistics (may be NULL) */
@@ -285,6 +305,21 @@ int of_flow_operator(of_ctx *ctx, const of_params *params, double alpha, const f
 /* _solve_linear_system (base.py:87-172) on the matrix-free operator */
 int of_solve(of_ctx *ctx, const of_params *params, const float *coef, const float *rhs, int H, int W,
              float *x, int *iters, double *rel_residual);
+/* General spatial_filters (params->filters.general): the operator in
+ * diagonal (DIA) form on the dense offset grid of radius D = max filter
+ * dimension - 1, G = (2D + 1)^2 offsets (di, dj) in row-major order
+ * (di = -D..D outer): planes = G planes of the u-u block, G of the v-v
+ * block, then the u-v coupling (offset 0); (A x)_u(i, j) = sum_o
+ * c_u,o(i, j) x_u(i + di, j + dj) + c_uv(i, j) x_v(i, j).  *D_out receives D
+ * (the caller sizes planes as (2 G + 1) H W floats, G from its own filters). */
+int of_flow_operator_dia(of_ctx *ctx, const of_params *params, double alpha, const float *uv,
+                         const float *duv, const float *It, const float *Ix, const float *Iy,
+                         int H, int W, int nc, int *D_out, float *planes, float *rhs);
+/* _solve_linear_system (base.py:87-172) on a DIA operator of radius D (any
+ * sparse A whose u-u / v-v blocks are 2-D stencils and whose u-v block is
+ * diagonal; the Python mirror converts scipy matrices) */
+int of_solve_dia(of_ctx *ctx, const of_params *params, int D, const float *planes, const float *rhs,
+                 int H, int W, float *x, int *iters, double *rel_residual);
 /* detect_occlusion (utils/occlusion.py:6-56) */
 int of_detect_occlusion(of_ctx *ctx, const float *uv, const float *images, int H, int W, int nc,
                         float *occ);

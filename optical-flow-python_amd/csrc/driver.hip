@@ -28,6 +28,7 @@
 #include "kernels_img.hip"
 #include "kernels_flow.hip"
 #include "kernels_solve.hip"
+#include "kernels_gen.hip"
 
 namespace {
 
@@ -1084,6 +1085,166 @@ SolveResult solve_tok(of_ctx *c, const of_params *P, const Img &coef, const F2 &
   return solve(c, P, coef, b, x);
 }
 
+// ---- general spatial_filters (kernels_gen.hip) ------------------------------
+// radius of the DIA offset grid: filters of fh x fw taps couple pixels up to
+// (fh - 1, fw - 1) apart
+int gen_radius(const of_params *P) {
+  int D = 0;
+  for (int q = 0; q < P->filters.n; ++q) D = std::max(D, std::max(P->filters.fh[q], P->filters.fw[q]) - 1);
+  return D;
+}
+int gen_nplanes(int D) { return 2 * (2 * D + 1) * (2 * D + 1) + 1; }
+
+GenFilters gen_filters(const of_params *P) {
+  GenFilters f;
+  memset(&f, 0, sizeof(f));
+  f.n = P->filters.n;
+  f.D = gen_radius(P);
+  for (int q = 0; q < f.n; ++q) {
+    f.fh[q] = P->filters.fh[q];
+    f.fw[q] = P->filters.fw[q];
+    for (int t = 0; t < f.fh[q] * f.fw[q]; ++t) f.taps[q][t] = (float)P->filters.taps[q][t];
+    f.ru[q] = to_penf(P->filters.rho_u[q]);
+    f.rv[q] = to_penf(P->filters.rho_v[q]);
+    f.qu[q] = to_penf(P->filters.qua_u[q]);
+    f.qv[q] = to_penf(P->filters.qua_v[q]);
+  }
+  return f;
+}
+
+// per-level buffers of the general path: filter weights, DIA planes, CG vectors
+struct GenLevel {
+  int D = 0;
+  Img w, pl;
+  F2 r, p, z, q, t, e;
+};
+GenLevel gen_level(of_ctx *c, const of_params *P, int H, int W) {
+  GenLevel L;
+  L.D = gen_radius(P);
+  L.w = new_img(c, H, W, std::max(1, 2 * P->filters.n));
+  L.pl = new_img(c, H, W, gen_nplanes(L.D));
+  L.r = new_f2(c, H, W);
+  L.p = new_f2(c, H, W);
+  L.z = new_f2(c, H, W);
+  L.q = new_f2(c, H, W);
+  L.t = new_f2(c, H, W);
+  L.e = new_f2(c, H, W);
+  return L;
+}
+
+void gen_flow_operator(of_ctx *c, const of_params *P, const OpArgs &o, const F2 &uv, const F2 *duv, const Img &It,
+                       const Img &Ix, const Img &Iy, const F2 *uvhat, const GenLevel &L, const F2 &rhs) {
+  const GenFilters f = gen_filters(P);
+  Grid2 g = grid2(uv.H, uv.W);
+  if (f.n)
+    launch(c, "gen_weights", k_gen_weights, g.grid, g.block, 0, f, o, (const float2 *)uv.p,
+           (const float2 *)(duv ? duv->p : nullptr), uv.H, uv.W, uv.P, L.w.ps(), L.w.p);
+  launch(c, "gen_dia", k_gen_dia, g.grid, g.block, 0, f, o, (const float *)L.w.p, (const float2 *)uv.p,
+         (const float2 *)(duv ? duv->p : nullptr), (const float *)It.p, (const float *)Ix.p, (const float *)Iy.p, It.C,
+         (const float2 *)(uvhat ? uvhat->p : nullptr), uv.H, uv.W, uv.P, L.pl.ps(), L.pl.p, rhs.p);
+}
+
+// CG on the DIA operator with the scipy control flow from x = 0; returns
+// (iterations, done)
+std::pair<int, int> dia_cg(of_ctx *c, DiaArgs a, int nb, Grid2 g) {
+  HIPCHK(hipMemsetAsync(a.st, 0, sizeof(PcgState), c->stream));
+  launch(c, "dia_init", k_dia_init, g.grid, g.block, 0, a);
+  int it = 0;
+  for (;;) {
+    const int n = std::min(32, a.maxiter + 1 - it);
+    for (int t = 0; t < n; ++t, ++it) {
+      launch(c, "dia_dir", k_dia_dir, g.grid, g.block, 0, a, it, nb);
+      launch(c, "dia_q", k_dia_q, g.grid, g.block, 0, a, it);
+      launch(c, "dia_upd", k_dia_upd, g.grid, g.block, 0, a, it, nb);
+    }
+    HIPCHK(hipMemcpyAsync(&c->h_state[0], a.st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_state[0].done || it > a.maxiter) break;
+  }
+  return {c->h_state[0].iter, c->h_state[0].done};
+}
+
+// _solve_linear_system (base.py:87-172) on a DIA operator
+SolveResult gen_solve(of_ctx *c, const of_params *P, const GenLevel &L, const F2 &b, const F2 &x) {
+  const int H = b.H, W = b.W;
+  DiaArgs a;
+  memset(&a, 0, sizeof(a));
+  a.pl = L.pl.p;
+  a.ps = L.pl.ps();
+  a.D = L.D;
+  a.H = H;
+  a.W = W;
+  a.P = b.P;
+  a.b = b.p;
+  a.x = x.p;
+  a.r = L.r.p;
+  a.p = L.p.p;
+  a.z = L.z.p;
+  a.q = L.q.p;
+  a.part = c->d_partials;
+  a.st = c->d_state;
+  const size_t vbytes = sizeof(float2) * (size_t)H * b.P;
+  if (P->solver == OF_SOLVER_SOR) {
+    HIPCHK(hipMemsetAsync(x.p, 0, vbytes, c->stream));
+    HIPCHK(hipMemsetAsync(a.st, 0, sizeof(PcgState), c->stream));
+    const int nt = std::min(1024, (W + 63) / 64 * 64);
+    launch(c, "dia_sor", k_dia_sor, dim3(1), dim3(nt), 0, a, (float)P->sor_omega, P->sor_max_iters, P->sor_tol);
+    HIPCHK(hipMemcpyAsync(&c->h_state[0], a.st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return {c->h_state[0].iter, c->h_state[0].done, 0.0};
+  }
+  REQUIRE(P->solver == OF_SOLVER_PCG || P->solver == OF_SOLVER_BACKSLASH, OF_EINVAL, "Unknown solver");
+  const bool bs = P->solver == OF_SOLVER_BACKSLASH;
+  a.block = bs;
+  Grid2 g = grid2(H, W, PCG_MAX_BLOCKS);
+  const int nb = g.nblocks;
+  // ||b||
+  {
+    launch(c, "norm2", k_norm2_part, g.grid, g.block, 0, (const float2 *)b.p, H, W, b.P, c->d_partials);
+    launch(c, "norm2", k_norm2_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_partials, nb, c->d_norm);
+    HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  const double bnorm = std::sqrt(*c->h_norm);
+  if (!bs) {
+    // scipy cg (base.py:116-136): Jacobi, rtol pcg_rtol, maxiter pcg_maxiter
+    a.atol = P->pcg_rtol * bnorm;
+    a.maxiter = P->pcg_maxiter;
+    const auto r = dia_cg(c, a, nb, g);
+    return {r.first, r.second, bnorm > 0 ? std::sqrt(c->h_state[0].rr) / bnorm : 0.0};
+  }
+  // 'backslash' surrogate: 2x2 block-Jacobi CG to exact_rtol, then iterative
+  // refinement x += CG(A, b - A x) on the fp64 true residual until it meets
+  // exact_rtol ||b|| (at most 4 corrections)
+  const double goal = P->exact_rtol * bnorm;
+  a.atol = 0.5 * goal;
+  a.maxiter = P->exact_maxiter;
+  auto r = dia_cg(c, a, nb, g);
+  int iters = r.first, done = r.second;
+  double rel = 0.0;
+  for (int ref = 0;; ++ref) {
+    DiaArgs t = a;
+    t.x = x.p;
+    launch(c, "dia_resid", k_dia_resid, g.grid, g.block, 0, t, L.t.p);
+    launch(c, "dia_sum", k_dia_sum, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)(c->d_partials + 8 * PCG_MAX_BLOCKS),
+           nb, c->d_norm);
+    HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const double tn = std::sqrt(*c->h_norm);
+    rel = bnorm > 0 ? tn / bnorm : 0.0;
+    if (tn <= goal || ref >= 4 || iters >= P->exact_maxiter) break;
+    DiaArgs e = a;
+    e.b = L.t.p;
+    e.x = L.e.p;
+    e.maxiter = P->exact_maxiter - iters;
+    r = dia_cg(c, e, nb, g);
+    iters += r.first;
+    done = r.second;
+    launch(c, "dia_acc", k_dia_acc, g.grid, g.block, 0, x.p, (const float2 *)L.e.p, H, W, b.P);
+  }
+  return {iters, rel <= P->exact_rtol ? 1 : done, rel};
+}
+
 // HSOpticalFlow.compute_flow_base (hs.py:109-142)
 void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
@@ -1125,11 +1286,19 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
   OpArgs o = op_args(P, alpha, 0.0);
   Grid2 g = grid2(H, W);
   const bool nl = P->method == OF_METHOD_CLASSIC_NL;
+  const bool gen = P->filters.general;
+  GenLevel GL;
+  if (gen) GL = gen_level(c, P, H, W);
   for (int it = 0; it < P->max_iters; ++it) {
     partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     for (int jl = 0; jl < max_linear; ++jl) {
-      flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
-      note_solve(c, st, solve_tok(c, P, coef, rhs, x));
+      if (gen) {
+        gen_flow_operator(c, P, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, GL, rhs);
+        note_solve(c, st, gen_solve(c, P, GL, rhs, x));
+      } else {
+        flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
+        note_solve(c, st, solve_tok(c, P, coef, rhs, x));
+      }
       c->cur_px = (double)H * W;
       const bool filt = P->median_filter_size != 0;
       launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
@@ -1169,6 +1338,9 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
   F2 rhs = new_f2(c, H, W), x = new_f2(c, H, W), duv = new_f2(c, H, W), t1 = new_f2(c, H, W), t2 = new_f2(c, H, W);
   Grid2 g = grid2(H, W);
   const int n = P->max_iters;
+  const bool gen = P->filters.general;
+  GenLevel GL;
+  if (gen) GL = gen_level(c, P, H, W);
   std::vector<double> l2s(n + 1);
   const double a = std::log10(1e-4), b = std::log10(P->lambda2);
   for (int t = 0; t < n; ++t) l2s[t] = std::pow(10.0, n == 1 ? a : a + (b - a) * t / (n - 1));
@@ -1179,8 +1351,13 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
     OpArgs o = op_args(P, alpha, lambda2);
     bool have_duv = false;
     for (int jl = 0; jl < P->max_linear; ++jl) {
-      flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
-      note_solve(c, st, solve_tok(c, P, coef, rhs, x));
+      if (gen) {
+        gen_flow_operator(c, P, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, GL, rhs);
+        note_solve(c, st, gen_solve(c, P, GL, rhs, x));
+      } else {
+        flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
+        note_solve(c, st, solve_tok(c, P, coef, rhs, x));
+      }
       c->cur_px = (double)H * W;
       // duv = clip(x): computed as (0 + clip(x))
       HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
@@ -1221,6 +1398,13 @@ void check_params(const of_params *P) {
   REQUIRE(P->median_filter_size == 0 || P->median_filter_size == 3 || P->median_filter_size == 5 ||
               P->median_filter_size == 7,
           OF_ENOTSUP, "median_filter_size must be None, 3, 5 or 7");
+  if (P->filters.general) {
+    REQUIRE(P->filters.n >= 0 && P->filters.n <= OF_MAX_FILTERS, OF_ENOTSUP, "at most 8 spatial filters");
+    for (int q = 0; q < P->filters.n; ++q)
+      REQUIRE(P->filters.fh[q] >= 1 && P->filters.fh[q] <= OF_MAX_FDIM && P->filters.fw[q] >= 1 &&
+                  P->filters.fw[q] <= OF_MAX_FDIM,
+              OF_ENOTSUP, "spatial filters of at most 5 x 5 taps");
+  }
 }
 
 // compute_flow (hs.py:49-99, ba.py:57-138, classic_nl.py:89-198, alt_ba.py:81-187)
@@ -2204,6 +2388,52 @@ int of_solve(of_ctx *c, const of_params *P, const float *coef, const float *rhs,
   API_END(c)
 }
 
+int of_flow_operator_dia(of_ctx *c, const of_params *P, double alpha, const float *uv, const float *duv,
+                         const float *It, const float *Ix, const float *Iy, int H, int W, int nc, int *D_out,
+                         float *planes, float *rhs) {
+  API_BEGIN(c)
+  REQUIRE(P && uv && It && Ix && Iy && planes && rhs && nc >= 1, OF_EINVAL, "bad arguments");
+  REQUIRE(P->filters.general, OF_EINVAL, "of_flow_operator_dia needs params->filters.general");
+  check_params(P);
+  F2 f = upload_f2(c, uv, H, W);
+  F2 df;
+  if (duv) df = upload_f2(c, duv, H, W);
+  Img a = new_img(c, H, W, nc), b = new_img(c, H, W, nc), d = new_img(c, H, W, nc);
+  upload_img(c, a, It);
+  upload_img(c, b, Ix);
+  upload_img(c, d, Iy);
+  GenLevel L = gen_level(c, P, H, W);
+  F2 r = new_f2(c, H, W);
+  gen_flow_operator(c, P, op_args(P, alpha, 0.0), f, duv ? &df : nullptr, a, b, d, nullptr, L, r);
+  download_img(c, L.pl, planes);
+  download_f2(c, r, rhs);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (D_out) *D_out = L.D;
+  API_END(c)
+}
+int of_solve_dia(of_ctx *c, const of_params *P, int D, const float *planes, const float *rhs, int H, int W, float *x,
+                 int *iters, double *rel_residual) {
+  API_BEGIN(c)
+  REQUIRE(P && planes && rhs && x && D >= 0 && D <= GEN_MAXD, OF_EINVAL, "bad arguments");
+  check_params(P);
+  GenLevel L;
+  L.D = D;
+  L.pl = new_img(c, H, W, gen_nplanes(D));
+  L.r = new_f2(c, H, W);
+  L.p = new_f2(c, H, W);
+  L.z = new_f2(c, H, W);
+  L.q = new_f2(c, H, W);
+  L.t = new_f2(c, H, W);
+  L.e = new_f2(c, H, W);
+  upload_img(c, L.pl, planes);
+  F2 b = upload_f2(c, rhs, H, W), xx = new_f2(c, H, W);
+  const SolveResult r = gen_solve(c, P, L, b, xx);
+  download_f2(c, xx, x);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (iters) *iters = r.iters;
+  if (rel_residual) *rel_residual = r.rel;
+  API_END(c)
+}
 int of_detect_occlusion(of_ctx *c, const float *uv, const float *images, int H, int W, int nc, float *occ) {
   API_BEGIN(c)
   REQUIRE(uv && images && occ && nc >= 1, OF_EINVAL, "bad arguments");

@@ -989,7 +989,7 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
     }
     rb ^= 1;
   };
-  double acc0 = 0.0, acc1 = 0.0;
+  double acc0 = 0.0;
 #pragma unroll
   for (int m = 0; m < CGR_M; ++m) acc0 += (double)(r[m].x * r[m].x + r[m].y * r[m].y);
   double rr, dummy;

@@ -6,7 +6,7 @@ share the exact struct layout.
 """
 import ctypes as C
 
-OF_ABI_VERSION = 2
+OF_ABI_VERSION = 3
 
 OF_OK, OF_EINVAL, OF_EHIP, OF_ENOMEM, OF_ENOTSUP, OF_ERCCL = 0, -1, -2, -3, -4, -5
 
@@ -38,13 +38,27 @@ _DBL_FIELDS = [
 ]
 
 
+MAX_FILTERS = 8
+MAX_FDIM = 5
+
+
+class OfFilterSet(C.Structure):
+    """of_filter_set: a general spatial_filters list (general = 0: the
+    default [[1, -1]], [[1], [-1]] pair)"""
+    _fields_ = [("general", C.c_int32), ("n", C.c_int32),
+                ("fh", C.c_int32 * MAX_FILTERS), ("fw", C.c_int32 * MAX_FILTERS),
+                ("taps", (C.c_double * (MAX_FDIM * MAX_FDIM)) * MAX_FILTERS),
+                ("rho_u", OfPenalty * MAX_FILTERS), ("rho_v", OfPenalty * MAX_FILTERS),
+                ("qua_u", OfPenalty * MAX_FILTERS), ("qua_v", OfPenalty * MAX_FILTERS)]
+
+
 class OfParams(C.Structure):
     _fields_ = ([(n, C.c_int32) for n in _INT_FIELDS]
                 + [(n, C.c_double) for n in _DBL_FIELDS]
                 + [("deriv_filter", C.c_double * 5),
                    ("rho_data", OfPenalty), ("rho_spatial_u", OfPenalty * 2), ("rho_spatial_v", OfPenalty * 2),
                    ("qua_data", OfPenalty), ("qua_spatial_u", OfPenalty * 2), ("qua_spatial_v", OfPenalty * 2),
-                   ("rho_couple", OfPenalty)])
+                   ("rho_couple", OfPenalty), ("filters", OfFilterSet)])
 
 
 class OfStats(C.Structure):

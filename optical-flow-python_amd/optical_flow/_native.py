@@ -61,6 +61,9 @@ _SIGS = {
     "of_flow_operator": ([_vp, C.POINTER(OfParams), C.c_double, _fp, _fp, _fp, _fp, _fp, C.c_int, C.c_int,
                           C.c_int, _fp, _fp], C.c_int),
     "of_solve": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, _fp, _ip, _dp], C.c_int),
+    "of_flow_operator_dia": ([_vp, C.POINTER(OfParams), C.c_double, _fp, _fp, _fp, _fp, _fp, C.c_int, C.c_int,
+                              C.c_int, _ip, _fp, _fp], C.c_int),
+    "of_solve_dia": ([_vp, C.POINTER(OfParams), C.c_int, _fp, _fp, C.c_int, C.c_int, _fp, _ip, _dp], C.c_int),
     "of_detect_occlusion": ([_vp, _fp, _fp, C.c_int, C.c_int, C.c_int, _fp], C.c_int),
     "of_weighted_median": ([_vp, _fp, _fp, C.c_int, _fp, C.c_int, C.c_int, C.c_int, C.c_double, _fp], C.c_int),
     "of_median_filter": ([_vp, _fp, C.c_int, C.c_int, C.c_int, C.c_int, _fp], C.c_int),

@@ -57,7 +57,7 @@ class AltBAOpticalFlow(BaseOpticalFlow):
     def _qua_penalties(self):
         """alt_ba.py:201-207: quadratic(1) everywhere."""
         one = _abi.penalty('quadratic', 1.0)
-        return one, [one, one], [one, one]
+        return one, [one for _ in self.rho_spatial_u], [one for _ in self.rho_spatial_v]
 
     def compute_flow_base(self, uv, uvhat):
         """One pyramid level with coupling and Li-Osher denoising

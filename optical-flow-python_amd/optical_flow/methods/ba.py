@@ -45,4 +45,5 @@ class BAOpticalFlow(BaseOpticalFlow):
         """ba.py:152-163: quadratic(1) spatial, quadratic(sigma_d / sigma_s) data."""
         ta = float(self.rho_data.param[0]) / float(self.rho_spatial_u[0].param[0])
         one = _abi.penalty('quadratic', 1.0)
-        return _abi.penalty('quadratic', ta), [one, one], [one, one]
+        return (_abi.penalty('quadratic', ta), [one for _ in self.rho_spatial_u],
+                [one for _ in self.rho_spatial_v])

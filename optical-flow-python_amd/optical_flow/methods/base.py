@@ -103,13 +103,30 @@ class BaseOpticalFlow(ABC):
     def _qua_penalties(self):
         raise NotImplementedError
 
+    def _general_filters(self):
+        """True when spatial_filters is not the default [[1, -1]], [[1], [-1]]
+        pair (the 5-point hot path); HS never uses spatial_filters (hs.py
+        assembles its own Laplacian)."""
+        if self._METHOD == 'hs':
+            return False
+        return len(self.spatial_filters) != 2 or any(
+            np.asarray(f).shape != d.shape or not np.array_equal(np.asarray(f), d)
+            for f, d in zip(self.spatial_filters, _DEFAULT_FILTERS))
+
     def _check_supported(self):
-        if len(self.spatial_filters) != 2 or any(
-                np.asarray(f).shape != d.shape or not np.array_equal(np.asarray(f), d)
-                for f, d in zip(self.spatial_filters, _DEFAULT_FILTERS)):
-            raise NotImplementedError("only the default spatial_filters [[1,-1]], [[1],[-1]] are supported")
-        if len(self.rho_spatial_u) != 2 or len(self.rho_spatial_v) != 2:
-            raise NotImplementedError("two spatial penalties per component are required")
+        if self._general_filters():
+            if len(self.spatial_filters) > _abi.MAX_FILTERS:
+                raise NotImplementedError(f"at most {_abi.MAX_FILTERS} spatial_filters are supported")
+            for f in self.spatial_filters:
+                f = np.atleast_2d(np.asarray(f, dtype=float))
+                if f.ndim != 2 or f.shape[0] > _abi.MAX_FDIM or f.shape[1] > _abi.MAX_FDIM:
+                    raise NotImplementedError(f"spatial filters of at most {_abi.MAX_FDIM} x {_abi.MAX_FDIM} taps")
+            if len(self.rho_spatial_u) < len(self.spatial_filters) or \
+                    len(self.rho_spatial_v) < len(self.spatial_filters):
+                # the reference indexes rho_spatial_u[i] per filter (classic_nl.py:315-316)
+                raise IndexError("rho_spatial_u / rho_spatial_v need one penalty per spatial filter")
+        elif len(self.rho_spatial_u) < 2 or len(self.rho_spatial_v) < 2:
+            raise IndexError("rho_spatial_u / rho_spatial_v need one penalty per spatial filter")
         if np.asarray(self.deriv_filter).size != 5:
             raise NotImplementedError("deriv_filter must have 5 taps")
 
@@ -176,13 +193,24 @@ class BaseOpticalFlow(ABC):
         for k, v in enumerate(np.asarray(self.deriv_filter, dtype=float).ravel()):
             P.deriv_filter[k] = v
         d, su, sv = self._robust_penalties()
-        P.rho_data = d
-        P.rho_spatial_u[0], P.rho_spatial_u[1] = su
-        P.rho_spatial_v[0], P.rho_spatial_v[1] = sv
         qd, qsu, qsv = self._qua_penalties()
+        P.rho_data = d
         P.qua_data = qd
-        P.qua_spatial_u[0], P.qua_spatial_u[1] = qsu
-        P.qua_spatial_v[0], P.qua_spatial_v[1] = qsv
+        for k in range(2):
+            if k < len(su):
+                P.rho_spatial_u[k], P.rho_spatial_v[k] = su[k], sv[k]
+                P.qua_spatial_u[k], P.qua_spatial_v[k] = qsu[k], qsv[k]
+        if self._general_filters():
+            F = P.filters
+            F.general = 1
+            F.n = len(self.spatial_filters)
+            for q, f in enumerate(self.spatial_filters):
+                f = np.atleast_2d(np.asarray(f, dtype=float))
+                F.fh[q], F.fw[q] = f.shape
+                for t, v in enumerate(f.ravel()):
+                    F.taps[q][t] = float(v)
+                F.rho_u[q], F.rho_v[q] = su[q], sv[q]
+                F.qua_u[q], F.qua_v[q] = qsu[q], qsv[q]
         rc = getattr(self, 'rho_couple', None)
         P.rho_couple = _abi.penalty_from_robust(rc) if rc is not None else _abi.penalty('charbonnier', 1e-3)
         return P
@@ -268,12 +296,38 @@ class BaseOpticalFlow(ABC):
             nat.ptr(nat.planar(Ix)), nat.ptr(nat.planar(Iy)), H, W, nc, nat.ptr(coef), nat.ptr(rhs)))
         return coef, rhs
 
+    def _operator_dia(self, uv, duv, It, Ix, Iy, alpha):
+        uv = np.asarray(uv, dtype=float)
+        H, W = uv.shape[:2]
+        It = np.asarray(It, dtype=float)
+        nc = 1 if It.ndim == 2 else It.shape[2]
+        P = self.to_params()
+        D = max([max(np.atleast_2d(f).shape) - 1 for f in self.spatial_filters] + [0])
+        planes = np.empty((dia_nplanes(D), H, W), dtype=np.float32)
+        rhs = np.empty((2, H, W), dtype=np.float32)
+        d_out = C.c_int(0)
+        ctx = nat.context()
+        ctx.check(ctx.lib.of_flow_operator_dia(
+            ctx.handle, C.byref(P), float(alpha), nat.ptr(nat.planar(uv)),
+            nat.ptr(None if duv is None else nat.planar(duv)), nat.ptr(nat.planar(It)),
+            nat.ptr(nat.planar(Ix)), nat.ptr(nat.planar(Iy)), H, W, nc, C.byref(d_out), nat.ptr(planes),
+            nat.ptr(rhs)))
+        assert d_out.value == D
+        return D, planes, rhs
+
     def flow_operator(self, uv, duv, It, Ix, Iy):
         """Assemble A, b on the GPU (matrix-free planes) and return them in the
         reference's scipy form: A (2N x 2N, Fortran-ordered [u; v]), b, None,
-        iterative (classic_nl.py:279-378, ba.py:208-302)."""
-        coef, rhs = self._operator_planes(uv, duv, It, Ix, Iy, 0.0 if self._METHOD == 'hs' else self._operator_alpha())
-        A = planes_to_sparse(coef)
+        iterative (classic_nl.py:279-378, ba.py:208-302).  A general
+        spatial_filters list comes back from the GPU in DIA form
+        (of_flow_operator_dia)."""
+        alpha = 0.0 if self._METHOD == 'hs' else self._operator_alpha()
+        if self._general_filters():
+            D, planes, rhs = self._operator_dia(uv, duv, It, Ix, Iy, alpha)
+            A = dia_to_sparse(planes, D)
+        else:
+            coef, rhs = self._operator_planes(uv, duv, It, Ix, Iy, alpha)
+            A = planes_to_sparse(coef)
         b = np.concatenate([rhs[0].ravel(order='F'), rhs[1].ravel(order='F')]).astype(float)
         quad = ('quadratic', 'gaussian')
         iterative = not all(r.method in quad for r in list(self.rho_spatial_u) + list(self.rho_spatial_v) + [self.rho_data])
@@ -286,7 +340,6 @@ class BaseOpticalFlow(ABC):
         """base.py:87-114 on the GPU: A must have the 5-point + 2x2-coupling
         structure that flow_operator produces."""
         H, W = int(uv_shape[0]), int(uv_shape[1])
-        coef = sparse_to_planes(A, H, W)
         bb = np.asarray(b, dtype=float)
         rhs = np.stack([bb[:H * W].reshape(H, W, order='F'), bb[H * W:].reshape(H, W, order='F')])
         P = self.to_params()
@@ -294,8 +347,16 @@ class BaseOpticalFlow(ABC):
         it = C.c_int(0)
         rr = C.c_double(0)
         ctx = nat.context()
-        ctx.check(ctx.lib.of_solve(ctx.handle, C.byref(P), nat.ptr(nat.f32(coef)), nat.ptr(nat.f32(rhs)), H, W,
-                                   nat.ptr(x), C.byref(it), C.byref(rr)))
+        try:
+            coef = sparse_to_planes(A, H, W)
+        except NotImplementedError:
+            # any other 2-D stencil operator (general spatial_filters): DIA form
+            D, planes = sparse_to_dia(A, H, W)
+            ctx.check(ctx.lib.of_solve_dia(ctx.handle, C.byref(P), D, nat.ptr(nat.f32(planes)),
+                                           nat.ptr(nat.f32(rhs)), H, W, nat.ptr(x), C.byref(it), C.byref(rr)))
+        else:
+            ctx.check(ctx.lib.of_solve(ctx.handle, C.byref(P), nat.ptr(nat.f32(coef)), nat.ptr(nat.f32(rhs)), H, W,
+                                       nat.ptr(x), C.byref(it), C.byref(rr)))
         # iterations (CG) / sweeps (SOR) and the solver's own residual estimate
         self.last_solve = {"iters": it.value, "rel_residual": rr.value}
         return nat.interleaved(x).reshape(uv_shape)
@@ -347,3 +408,72 @@ def sparse_to_planes(A, H, W):
     if abs(R - A).max() > 1e-9 * max(1.0, abs(A).max()):
         raise NotImplementedError("A is not a symmetric 5-point + 2x2-coupling flow operator")
     return coef
+
+
+def dia_nplanes(D):
+    """planes of the DIA operator of radius D: G u-u, G v-v, 1 u-v (G = (2D+1)^2)"""
+    return 2 * (2 * D + 1) ** 2 + 1
+
+
+def dia_to_sparse(planes, D):
+    """DIA planes (include/optflow.h, of_flow_operator_dia) -> scipy CSC with
+    the reference's ordering (k = j*H + i, u block then v block)."""
+    planes = np.asarray(planes, dtype=float)
+    _, H, W = planes.shape
+    N = H * W
+    S = 2 * D + 1
+    G = S * S
+    k = np.arange(N).reshape(W, H).T
+    rows, cols, vals = [], [], []
+    for comp in range(2):
+        o = comp * N
+        for di in range(-D, D + 1):
+            for dj in range(-D, D + 1):
+                c = planes[comp * G + (di + D) * S + (dj + D)]
+                i0, i1 = max(0, -di), min(H, H - di)
+                j0, j1 = max(0, -dj), min(W, W - dj)
+                if i0 >= i1 or j0 >= j1:
+                    continue
+                blk = c[i0:i1, j0:j1]
+                nz = blk != 0
+                rows.append(o + k[i0:i1, j0:j1][nz])
+                cols.append(o + k[i0 + di:i1 + di, j0 + dj:j1 + dj][nz])
+                vals.append(blk[nz])
+    cuv = planes[2 * G]
+    nz = cuv != 0
+    rows += [k[nz], N + k[nz]]
+    cols += [N + k[nz], k[nz]]
+    vals += [cuv[nz], cuv[nz]]
+    return sparse.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                             shape=(2 * N, 2 * N))
+
+
+def sparse_to_dia(A, H, W):
+    """Inverse of dia_to_sparse for any A whose u-u and v-v blocks are 2-D
+    stencils of radius <= 4 and whose u-v block is diagonal; raises
+    NotImplementedError otherwise.  Returns (D, planes)."""
+    N = H * W
+    A = sparse.coo_matrix(A)
+    if A.shape != (2 * N, 2 * N):
+        raise ValueError(f"A has shape {A.shape}, expected {(2 * N, 2 * N)}")
+    r, c, v = A.row, A.col, A.data
+    rc, cc = r // N, c // N
+    ri, rj = (r % N) % H, (r % N) // H
+    ci, cj = (c % N) % H, (c % N) // H
+    di, dj = ci - ri, cj - rj
+    same = rc == cc
+    if np.any(~same & ((di != 0) | (dj != 0))):
+        raise NotImplementedError("A's u-v block is not diagonal")
+    D = int(max(np.abs(di).max(initial=0), np.abs(dj).max(initial=0)))
+    if D > 4:
+        raise NotImplementedError("A couples pixels more than 4 apart")
+    S = 2 * D + 1
+    G = S * S
+    planes = np.zeros((dia_nplanes(D), H, W))
+    e = np.where(same, rc * G + (di + D) * S + (dj + D), 2 * G)
+    keep = same | (rc == 0)  # the u-v coupling once, from the u rows
+    np.add.at(planes, (e[keep], ri[keep], rj[keep]), v[keep])
+    R = dia_to_sparse(planes, D)
+    if abs(R - A).max() > 1e-9 * max(1.0, abs(A).max()):
+        raise NotImplementedError("A is not a 2-D stencil operator of the flow system's form")
+    return D, planes

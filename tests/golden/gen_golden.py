@@ -435,6 +435,83 @@ def gen_viz_metrics():
     save("viz_metrics.npz", **out)
 
 
+FILTER_SETS = {
+    # 4-neighbour + both diagonals, first differences
+    "diag4": [np.array([[1, -1]]), np.array([[1], [-1]]), np.array([[1, 0], [0, -1]]), np.array([[0, 1], [-1, 0]])],
+    # second differences (3 taps, 'sameswap' offset 1)
+    "wide": [np.array([[1, -2, 1]]), np.array([[1], [-2], [1]])],
+    # a single horizontal filter
+    "one": [np.array([[1, -1]])],
+}
+
+
+def gen_filters():
+    """General spatial_filters (classic_nl.py:301-322, ba.py:228-246): the
+    reference's flow_operator (A as COO, b) for three filter lists on a
+    48x64 level with a smooth uv / duv and random-smooth derivatives, its
+    lexicographic SOR on the diag4 operator, and estimate_flow end to end on
+    the RubberWhale crop (classic+nl-fast with diag4, classic-c with wide and
+    'pcg')."""
+    from optical_flow.methods.base import BaseOpticalFlow
+    from scipy import sparse
+    from scipy.ndimage import gaussian_filter
+    im1, im2 = rubberwhale()
+    c1 = im1[150:198, 250:314].copy()
+    c2 = im2[150:198, 250:314].copy()
+    out = {"im1": c1, "im2": c2}
+    H, W = c1.shape[:2]
+    rng = np.random.default_rng(23)
+    yy, xx = np.mgrid[0:H, 0:W]
+    uv0 = np.stack([0.6 * np.sin(xx / 9.0) + 0.2, 0.4 * np.cos(yy / 7.0) - 0.1], axis=2)
+    duv0 = 0.05 * np.stack([gaussian_filter(rng.standard_normal((H, W)), 2) for _ in range(2)], axis=2)
+    der = [gaussian_filter(rng.standard_normal((H, W)), 1.5) * s for s in (8.0, 20.0, 20.0)]
+    # float32-representable inputs: the GPU assembles in float32, and steep
+    # robust weights would otherwise compare input rounding, not arithmetic
+    f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
+    uv0, duv0, der = f32(uv0), f32(duv0), [f32(a) for a in der]
+    out["uv"], out["duv"], out["It"], out["Ix"], out["Iy"] = uv0, duv0, der[0], der[1], der[2]
+    # operator level: 'wide' with BA's Lorentzian (classic-c's Charbonnier(1e-3)
+    # weights jump by ~10 % between neighbouring float32 values of a
+    # second difference near 0); end to end below it runs with classic-c
+    for tag, meth in (("diag4", "classic+nl-fast"), ("wide", "ba"), ("one", "classic+nl-fast")):
+        o = ref_cfg.load_of_method(meth)
+        n = len(FILTER_SETS[tag])
+        o.spatial_filters = FILTER_SETS[tag]
+        o.rho_spatial_u = [o.rho_spatial_u[i % 2] for i in range(n)]
+        o.rho_spatial_v = [o.rho_spatial_v[i % 2] for i in range(n)]
+        for dtag, duv in (("", None), ("_duv", duv0)):
+            A, b, _, _ = o.flow_operator(uv0, np.zeros_like(uv0) if duv is None else duv, der[0], der[1], der[2])
+            A = sparse.coo_matrix(A)
+            out[f"op_{tag}{dtag}_row"], out[f"op_{tag}{dtag}_col"] = A.row, A.col
+            out[f"op_{tag}{dtag}_val"], out[f"op_{tag}{dtag}_b"] = A.data, b
+    A = sparse.coo_matrix((out["op_diag4_val"], (out["op_diag4_row"], out["op_diag4_col"])),
+                          shape=(2 * H * W, 2 * H * W)).tocsr()
+    calls = [0]
+    norm = np.linalg.norm
+
+    def counting_norm(*a, **k):
+        calls[0] += 1
+        return norm(*a, **k)
+    np.linalg.norm = counting_norm
+    try:
+        out["sor_diag4_x"] = BaseOpticalFlow._sor_solve(None, A, out["op_diag4_b"], 1.9, 10000, 1e-2)
+    finally:
+        np.linalg.norm = norm
+    out["sor_diag4_sweeps"] = np.array(calls[0] // 2)
+    out["spsolve_diag4_x"] = spsolve(A.tocsc(), out["op_diag4_b"])
+    for tag, meth, extra in (("diag4", "classic+nl-fast", {}), ("wide", "classic-c", {"solver": "pcg"})):
+        o = ref_cfg.load_of_method(meth)
+        n = len(FILTER_SETS[tag])
+        prm = {"spatial_filters": FILTER_SETS[tag],
+               "rho_spatial_u": [o.rho_spatial_u[i % 2] for i in range(n)],
+               "rho_spatial_v": [o.rho_spatial_v[i % 2] for i in range(n)]}
+        prm.update(extra)
+        t0 = time.time()
+        out[f"e2e_{tag}"] = quiet(ref.estimate_flow, c1, c2, meth, prm)
+        print(f"  e2e {tag} {meth}: {time.time() - t0:.1f}s")
+    save("filters.npz", **out)
+
+
 if __name__ == "__main__":
     jobs = sys.argv[1:] or ["unit", "e2e_small", "e2e_synth"]
     for j in jobs:

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert set(syms) == set(_native.EXPORTED_SYMBOLS)
-    assert lib.of_abi_version() == 2
+    assert lib.of_abi_version() == 3
 
 
 def test_struct_layout_matches_header():
@@ -39,8 +39,9 @@ def test_struct_layout_matches_header():
     from optical_flow import _abi
     import subprocess
     import tempfile
-    src = ('#include "optflow.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%zu %zu %zu %zu\\n",'
-           'sizeof(of_params), sizeof(of_stats), offsetof(of_params, rho_couple), offsetof(of_params, lambda_));}\n')
+    src = ('#include "optflow.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%zu %zu %zu %zu %zu %zu\\n",'
+           'sizeof(of_params), sizeof(of_stats), offsetof(of_params, rho_couple), offsetof(of_params, lambda_),'
+           'offsetof(of_params, filters), sizeof(of_filter_set));}\n')
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
         open(c, "w").write(src)
@@ -50,6 +51,8 @@ def test_struct_layout_matches_header():
     assert int(out[1]) == ctypes.sizeof(_abi.OfStats)
     assert int(out[2]) == _abi.OfParams.rho_couple.offset
     assert int(out[3]) == _abi.OfParams.lambda_.offset
+    assert int(out[4]) == _abi.OfParams.filters.offset
+    assert int(out[5]) == ctypes.sizeof(_abi.OfFilterSet)
 
 
 def test_no_cpu_fallback_without_library(monkeypatch):
@@ -108,7 +111,10 @@ def test_params_flattening():
     with pytest.raises(ValueError, match="Unknown solver"):
         o.to_params()
     o = load_of_method("ba")
-    o.spatial_filters = [np.array([[1, -2, 1]])]
+    o.spatial_filters = [np.array([[1, -2, 1]])]  # general lists run (kernels_gen.hip)
+    P = o.to_params()
+    assert P.filters.general == 1 and P.filters.n == 1 and (P.filters.fh[0], P.filters.fw[0]) == (1, 3)
+    o.spatial_filters = [np.ones((1, 6))]  # beyond 5 x 5 taps
     with pytest.raises(NotImplementedError):
         o.to_params()
 
