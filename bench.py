@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=8, help="pairs per GPU per step (config 5: 64 pairs / 8 GPUs)")
-    ap.add_argument("--lanes", type=int, default=3, help="concurrent pair pipelines per GPU (of_pairs_run_host)")
+    ap.add_argument("--lanes", type=int, default=4, help="concurrent pair pipelines per GPU (of_pairs_run_host)")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--method", default="classic+nl-fast")

@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <immintrin.h>
 #include <cmath>
 #include <cstdio>
@@ -48,6 +49,29 @@ struct OfError {
   } while (0)
 
 // grow-only device arena: chunks are kept across calls, offsets reset per call
+// the lanes' token for fine CG solves (BigPhase below): OF_TOKEN_SLOTS
+// solves may hold it at once
+#ifndef OF_TOKEN_SLOTS
+#define OF_TOKEN_SLOTS 2
+#endif
+struct Token {
+  std::mutex m;
+  std::condition_variable cv;
+  int free = OF_TOKEN_SLOTS;
+  void lock() {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [&] { return free > 0; });
+    --free;
+  }
+  void unlock() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      ++free;
+    }
+    cv.notify_one();
+  }
+};
+
 struct Arena {
   struct Chunk {
     char *p;
@@ -181,8 +205,8 @@ struct of_ctx {
   std::vector<Slot> slots;
   HostStage *hs = nullptr;      // of_pairs_run_host staging (lazily created)
   std::vector<of_ctx *> lanes;  // of_pairs_run pipelines: own stream, arena and solver state
-  std::mutex big_own;           // (parent) the big-phase token its lanes share
-  std::mutex *big = nullptr;    // (lane) token held through phases of >= big_px pixels
+  Token big_own;                // (parent) the big-phase token its lanes share
+  Token *big = nullptr;         // (lane) token held through phases of >= big_px pixels
   double big_px = 0;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -700,14 +724,30 @@ void cheb_poly(int m, double a, double b, double *cB) {
 #ifndef CGS_MIN_R
 #define CGS_MIN_R 8
 #endif
-int cg_geometry(int H, int W, bool split, of_cg_geometry *g) {
+// k_cgs blocks of a fine solve in lanes mode, where OF_TOKEN_SLOTS (2) fine
+// solves of different pairs run side by side: one block per CU each, so a
+// band is twice as tall (R = 78 at 1080p) and walks R + 19 row steps for R
+// rows instead of 39 + 19 (the band halo is recomputed once per band).
+// Measured (round 3, 2 x 2 reps): 1 slot x 504 blocks 38.9, 2 x 504 40.7,
+// 2 x 336 42.8, 2 x 252 44.4 (4 lanes: 45.3), 2 x 200 42.9, 3 x 168 45.0,
+// 4 x 128 42.6 pairs/s (profiles/r3y_token_slots_ab.log, r3z_ab.log)
+#ifndef CGS_LANES_BLOCKS
+#define CGS_LANES_BLOCKS 252
+#endif
+// k_cgs blocks of the other (coarse) solves in lanes mode: 128 / 252 measured
+// +1 % (45.3 / 45.2 vs 44.8 pairs/s, profiles/r3aa_coarse_blocks_ab.log) but
+// would make batches of sub-Mpx pairs differ from estimate_flow; kept at 504
+#ifndef CGS_LANES_COARSE_BLOCKS
+#define CGS_LANES_COARSE_BLOCKS CGS_TARGET_BLOCKS
+#endif
+int cg_geometry(int H, int W, bool split, of_cg_geometry *g, int target_blocks = CGS_TARGET_BLOCKS) {
   if (H < 1 || W < 1) return OF_EINVAL;
   const int sw = split ? PCG_SWP : PCG_SW;
   const int nstrips = (W + sw - 1) / sw;
   if (nstrips > PCG_MAX_BLOCKS) return OF_ENOTSUP;
   int nbands, R, gy;
   if (split) {
-    nbands = std::max(1, std::min((H + CGS_MIN_R - 1) / CGS_MIN_R, CGS_TARGET_BLOCKS / nstrips));
+    nbands = std::max(1, std::min((H + CGS_MIN_R - 1) / CGS_MIN_R, target_blocks / nstrips));
     R = (H + nbands - 1) / nbands;
     nbands = (H + R - 1) / R;
     gy = nbands;
@@ -825,7 +865,9 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     // block's 4 waves); 'pcg': scipy's Jacobi CG in k_cg
     const bool split = block;
     of_cg_geometry geo;
-    const int gst = cg_geometry(H, W, split, &geo);
+    const bool lanes_fine = c->big && (double)H * W >= c->big_px;  // a token-holding solve
+    const int gst = cg_geometry(H, W, split, &geo,
+                                lanes_fine ? CGS_LANES_BLOCKS : c->big ? CGS_LANES_COARSE_BLOCKS : CGS_TARGET_BLOCKS);
     REQUIRE(gst == OF_OK, gst, "level too wide for the fused CG kernels");
     REQUIRE(coef.ps() * 7 * 4 < 0x40000000ull, OF_ENOTSUP, "level too large for the CG kernels");
     const dim3 grid(geo.grid_x, geo.grid_y), blk(OF_BX, OF_BY);
@@ -1046,11 +1088,15 @@ struct LevelIn {
 };
 
 // Lanes mode (of_pairs_run, of_pairs_run_host): every linear solve on a
-// level of >= big_px pixels (solve_tok below) holds the lanes' shared token
-// until its GPU work has drained, so at most one pair at a time streams a fine CG working set
-// (1080p: ~190 MB, most of the 256 MB Infinity Cache) and two lanes' 512-block
-// CG launches never interleave.  Warps, assembly and the weighted median of
-// fine levels run unserialised.  Tried and rejected (round 3): the token
+// level of >= big_px pixels (solve_tok below) holds one of the lanes' token
+// slots (OF_TOKEN_SLOTS = 2) until its GPU work has drained, and runs its
+// k_cgs launches with CGS_LANES_BLOCKS (252, one per CU) blocks, so two fine
+// solves of different pairs fill the chip side by side with bands twice as
+// tall as one solve's 504 blocks would have.  Until round 3 the token had one
+// slot and a fine solve 504 blocks (two lanes' 504-block launches
+// interleaving at block granularity stall each other: 2 slots x 504 blocks is
+// only +4 %).  Warps, assembly and the weighted median of fine levels run
+// unserialised.  Tried and rejected (round 3): the token
 // holder's solve on a shared high-priority stream, 32.3-32.8 vs 35.5-36.2
 // pairs/s (profiles/r3f_cg_priority_ab.log).  Outside lanes mode: no-op.
 // The full-size preprocessing (ROF, pyramids) ran under the token through

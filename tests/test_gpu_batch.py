@@ -137,3 +137,26 @@ def test_pairs_run_host_matches_estimate_flow(lanes, n, H, W):
     assert np.array_equal(np.moveaxis(uv, 0, 2), got[n - 1])
     with pytest.raises(ValueError):
         optical_flow.estimate_flow_batch([a[0] + 0.5], [b[0]])
+
+
+def test_pairs_run_host_fine_solves_side_by_side():
+    """Lanes mode at 1080p: two fine solves hold the token's two slots at
+    once, each with 252 k_cgs blocks (CGS_LANES_BLOCKS) instead of a single
+    estimate_flow's 504, so the band geometry and the CG partial-sum order
+    differ; both meet the 1e-6 true residual, so the flows agree to CG
+    rounding (measured below), and lane counts >= 2 agree bitwise."""
+    import optical_flow
+    from optical_flow.utils.synthetic import synth_pair
+    pairs = [synth_pair(1080, 1920, 40 + k) for k in range(3)]
+    a = [p[0].astype(np.uint8) for p in pairs]
+    b = [p[1].astype(np.uint8) for p in pairs]
+    got2 = optical_flow.estimate_flow_batch(a, b, "classic+nl-fast", lanes=2)
+    got3 = optical_flow.estimate_flow_batch(a, b, "classic+nl-fast", lanes=3)
+    for k in range(3):
+        assert np.array_equal(got2[k], got3[k]), k
+    ref = optical_flow.estimate_flow(pairs[0][0], pairs[0][1], "classic+nl-fast")
+    e = np.sqrt(((got2[0] - ref) ** 2).sum(-1))
+    aepe = lambda uv: float(np.sqrt(((uv - pairs[0][2]) ** 2).sum(-1)).mean())  # noqa: E731
+    print(f"lanes vs single 1080p: mean {e.mean():.2e} p99 {np.percentile(e, 99):.2e} "
+          f"dAEPE {abs(aepe(got2[0]) - aepe(ref)):.2e}")
+    assert e.mean() < 1e-3 and abs(aepe(got2[0]) - aepe(ref)) < 1e-4
