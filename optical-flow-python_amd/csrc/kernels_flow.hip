@@ -395,6 +395,21 @@ extern __device__ unsigned long long g_wmf_t[];
 #define WMF_STAMP(i)
 #endif
 #define WMF_NC 8
+// chunk-sum type: fp64 (default, 100 % exact on every fixture) or fp32
+// (WMF_F32SUM: half the chunk-sum LDS).  The fp32 build emits native
+// ds_add_f32 (checked in the ISA, no CAS loop) and yet runs 4.93 vs 0.83 ms
+// per 1080p launch (99.996 % exact at h = 12; profiles/r3ac_wmf_f32sum.log):
+// on gfx950 the fp32 LDS add is far slower than ds_add_f64 here.  Off.
+#ifndef WMF_F32SUM
+#define WMF_F32SUM 0
+#endif
+#if WMF_F32SUM
+typedef float wmf_sum_t;
+#define WMF_SUM_SHIFT 8
+#else
+typedef double wmf_sum_t;
+#define WMF_SUM_SHIFT 9
+#endif
 template <int GC>
 struct WmfRec;
 template <>
@@ -549,7 +564,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // [RW][RP] | sorted positions (ry << 8 | rx) of the u and v lists [2][N] u16 |
   // chunk ids [2][RW][RP] u8 (u list, v list)
   extern __shared__ double lds_f64[];
-  double *csum = lds_f64;
+  wmf_sum_t *csum = reinterpret_cast<wmf_sum_t *>(lds_f64);
   T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
   uint16_t *ku = reinterpret_cast<uint16_t *>(smp + RW * RP), *kv = ku + N;
   uint8_t *cid = reinterpret_cast<uint8_t *>(kv + N);
@@ -575,7 +590,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       smp[ry * RP + rx] = WmfRec<GC>::make(gv[0], gv[1], gv[2], occ[g]);
     }
   }
-  double *cs = csum + lane;
+  wmf_sum_t *cs = csum + lane;
 #pragma unroll
   for (int c = 0; c < 2 * WMF_NC; ++c) cs[c * 64] = 0.0;
   WMF_STAMP(1);
@@ -620,9 +635,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int dx = 0; dx < MX; ++dx)
       if (dx < n) {
-        const double w = (double)wmf_w(rec[dx], c01, cg[2], nk);
-        atomicAdd(reinterpret_cast<double *>(csb + (cu[dx] << 9)), w);
-        atomicAdd(reinterpret_cast<double *>(csb + (cv[dx] << 9)) + WMF_NC * 64, w);
+        const wmf_sum_t w = (wmf_sum_t)wmf_w(rec[dx], c01, cg[2], nk);
+        atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cu[dx] << WMF_SUM_SHIFT)), w);
+        atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
       }
   };
   if (HS > 0) {
