@@ -480,29 +480,40 @@ __global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands)
 
 // ---------------------------------------------------------------------------
 // The 'backslash' surrogate iteration (k_cgs below): the fused, q-free CG
-// iteration with a degree-3 polynomial preconditioner in the 2x2
+// iteration with a degree-CG_DEG (5) polynomial preconditioner in the 2x2
 // block-Jacobi splitting A = D - N, B = D^-1 N:
-//   M^-1 = (c0 + c1 B + c2 B^2 + c3 B^3) D^-1,
+//   M^-1 = (c0 + c1 B + ... + c5 B^5) D^-1,
 // the Chebyshev polynomial that minimises max |1 - X p(X)| for the spectrum
-// of X = D^-1 A = I - B on [0.04, 2] (host: cheb_poly; 2 bounds the
-// spectrum because D + N is positive semidefinite).  p > 0 there, so M is
-// SPD.  Measured on Classic+NL stage-2 systems (RubberWhale, 1e-6 relative
-// residual): 0.54x the iterations of a first-order Neumann preconditioner,
-// 0.27x of block Jacobi.
+// of X = D^-1 A = I - B on [a, 2] (a = 0.04, 0.02 for the robust GNC stages;
+// host: cheb_poly; 2 bounds the spectrum because D + N is positive
+// semidefinite).  p > 0 there, so M is SPD.  (Round 1 used degree 3: 0.54x
+// the iterations of a first-order Neumann preconditioner, 0.27x of block
+// Jacobi; degree 5 takes 0.69x the iterations of degree 3.)
 //
 // z = M^-1 r by Horner, one neighbour exchange per stage:
-//   y = D^-1 r,  g2 = c2 y + c3 D^-1 N y,  g1 = c1 y + D^-1 N g2,
+//   y = D^-1 r,  g4 = c4 y + c5 D^-1 N y,  g3 = c3 y + D^-1 N g4, ...,
 //   z = c0 y + D^-1 N g1   (and r.z = c0 r.y + y.N g1).
 // The rho recurrence needs q.M^-1 q = sum_i c_i T_i with y_q = D^-1 q,
-// v1 = D^-1 N y_q:  T0 = y_q.q, T1 = y_q.N y_q, T2 = v1.N y_q (= v1.D v1),
-// T3 = v1.N v1 (each edge counted once, by its right / lower pixel).
+// v1 = D^-1 N y_q, v2 = D^-1 N v1:  T0 = y_q.q, T1 = y_q.N y_q, T2 = v1.N y_q,
+// T3 = v1.N v1, T4 = v2.N v1, T5 = v2.N v2 (each edge counted once, by its
+// right / lower pixel).
 // Seven stencil stages deep, so a strip carries four halo lanes per side
 // (PCG_SWP = 112 output columns, lanes 4..59).  Arithmetic is on (u, v)
 // pairs of one pixel (packed fp32: v_pk_fma_f32).  Each row's coefficients
 // are staged once into an LDS ring of records (per pixel the (u, v) weight
 // pairs of the edges right and below and D^-1 as (ia, ic), (ic, id)) that
 // every stage reads; D itself is re-formed from D^-1 where a stage needs it.
-#define PCG_SWP 112
+// halo lanes per side of a k_cgs strip (2 px each).  Everything a launch
+// stores (r, p, x) and the dots p.q, q.z, r.z, r.r are exact with 4 (z
+// reaches 6 px out); only the T terms of q.M^-1 q at the strip's first and
+// last output columns reach 9-10 px (T5 uses v2 of the left neighbour), so
+// they see the DPP's zero beyond lane 0.  That moves only the rho
+// recurrence's beta: 5 halo lanes (108 output columns) give the same 479 CG
+// iterations per 1080p pair and the same pairs/s (profiles/r3ae_*), so 4.
+#ifndef CGS_HALO
+#define CGS_HALO 4
+#endif
+#define PCG_SWP (128 - 4 * CGS_HALO)
 #define CG_ROW_OOB 0x40000000u
 
 struct CgRec {  // one LDS-ring row: pixel e of the lane, (u, v) pairs
@@ -1195,9 +1206,9 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   // co-resident blocks differently on the SIMDs, role = wid ^ f(block), was
   // no faster: 51.5-54 vs 52 us per 1080p launch)
   const int role = wid;
-  const int jc = (tile - band * gridDim.x) * PCG_SWP - 8 + 2 * lane;
+  const int jc = (tile - band * gridDim.x) * PCG_SWP - 2 * CGS_HALO + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
-  const bool out_lane = lane >= 4 && lane <= 59;
+  const bool out_lane = lane >= CGS_HALO && lane < 64 - CGS_HALO;
   const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
   const unsigned soff8 = ok0 && out_lane ? (unsigned)jc * 8u : CG_OOB;
   const bool live = band < nbands;
