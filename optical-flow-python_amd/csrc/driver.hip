@@ -734,6 +734,12 @@ void cheb_poly(int m, double a, double b, double *cB) {
 #ifndef CGS_LANES_BLOCKS
 #define CGS_LANES_BLOCKS 252
 #endif
+// ... of a fine solve below 1.5 Mpx (864 x 1536, stage 2's first level):
+// 168 / 196 / 336 measured 43.6 / 44.0 / 43.6 vs 44.9 pairs/s at 252
+// (profiles/r3af_864_blocks_ab.log)
+#ifndef CGS_LANES_BLOCKS_S
+#define CGS_LANES_BLOCKS_S CGS_LANES_BLOCKS
+#endif
 // k_cgs blocks of the other (coarse) solves in lanes mode: 128 / 252 measured
 // +1 % (45.3 / 45.2 vs 44.8 pairs/s, profiles/r3aa_coarse_blocks_ab.log) but
 // would make batches of sub-Mpx pairs differ from estimate_flow; kept at 504
@@ -866,8 +872,9 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     const bool split = block;
     of_cg_geometry geo;
     const bool lanes_fine = c->big && (double)H * W >= c->big_px;  // a token-holding solve
+    const int lanes_target = (double)H * W >= 1.5 * (1 << 20) ? CGS_LANES_BLOCKS : CGS_LANES_BLOCKS_S;
     const int gst = cg_geometry(H, W, split, &geo,
-                                lanes_fine ? CGS_LANES_BLOCKS : c->big ? CGS_LANES_COARSE_BLOCKS : CGS_TARGET_BLOCKS);
+                                lanes_fine ? lanes_target : c->big ? CGS_LANES_COARSE_BLOCKS : CGS_TARGET_BLOCKS);
     REQUIRE(gst == OF_OK, gst, "level too wide for the fused CG kernels");
     REQUIRE(coef.ps() * 7 * 4 < 0x40000000ull, OF_ENOTSUP, "level too large for the CG kernels");
     const dim3 grid(geo.grid_x, geo.grid_y), blk(OF_BX, OF_BY);
