@@ -54,7 +54,7 @@ def _as_u8(im):
     return np.ascontiguousarray(f.astype(np.uint8))
 
 
-def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes=2):
+def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes=4):
     """estimate_flow over a batch of uint8 frame pairs, host to host: one C
     call (of_pairs_run_host) keeps `lanes` pairs in flight on the GPU with
     their uploads and downloads overlapped.  Returns a list of (H, W, 2)

@@ -87,7 +87,7 @@ def _finish(job, uv, gt, border):
     return res
 
 
-def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=3, chunk=8, workers=4, writers=2, border=0,
+def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, workers=4, writers=2, border=0,
                  keep_flows=False, flow_fn=None):
     """Run `jobs` (PairJob list) through decode -> flow -> write + metrics
     with the three stages overlapped.  Returns (results, stats): one dict

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=16)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--lanes", type=int, default=3)
+    ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--chunk", type=int, default=8)
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--writers", type=int, default=3)
