@@ -161,6 +161,8 @@ struct HostStage {
 struct of_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t hp = nullptr;  // high-priority stream of fine solves (OF_SOLVE_PRIO)
+  hipEvent_t ev_hp[2] = {nullptr, nullptr};
   std::string err;
   Arena arena;
   PcgState *d_state = nullptr, *h_state = nullptr;  // h_state: 2 pinned slots
@@ -1133,9 +1135,36 @@ struct BigPhase {
 // weighted median (VALU/LDS-bound) overlap another lane's CG (issue- and
 // HBM-bound); measured 33.8 -> 34.5 pairs/s at 3 lanes vs holding the token
 // through whole fine levels
+// OF_SOLVE_PRIO: a token-holding solve runs on its lane's high-priority
+// stream, so its blocks are dispatched ahead of other lanes' kernels as CUs
+// free up (a 252-block k_cgs launch needs 74 KB of LDS per CU, which the
+// weighted median's 19 KB waves otherwise keep refilling)
+#ifndef OF_SOLVE_PRIO
+#define OF_SOLVE_PRIO 0
+#endif
 SolveResult solve_tok(of_ctx *c, const of_params *P, const Img &coef, const F2 &b, const F2 &x) {
   BigPhase bp(c, (double)b.H * b.W);
-  return solve(c, P, coef, b, x);
+  if (!(OF_SOLVE_PRIO && bp.held)) return solve(c, P, coef, b, x);
+  if (!c->hp) {
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&c->hp, hipStreamNonBlocking, greatest));
+    for (auto &e : c->ev_hp) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  HIPCHK(hipEventRecord(c->ev_hp[0], c->stream));
+  HIPCHK(hipStreamWaitEvent(c->hp, c->ev_hp[0], 0));
+  std::swap(c->stream, c->hp);
+  SolveResult r;
+  try {
+    r = solve(c, P, coef, b, x);
+  } catch (...) {
+    std::swap(c->stream, c->hp);
+    throw;
+  }
+  std::swap(c->stream, c->hp);
+  HIPCHK(hipEventRecord(c->ev_hp[1], c->hp));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_hp[1], 0));
+  return r;
 }
 
 // ---- general spatial_filters (kernels_gen.hip) ------------------------------
@@ -1734,6 +1763,12 @@ int of_ctx_destroy(of_ctx *c) {
   hipFree(c->d_mm);
   hipFree(c->d_norm);
   hipHostFree(c->h_norm);
+  if (c->hp) {
+    hipStreamSynchronize(c->hp);
+    hipStreamDestroy(c->hp);
+  }
+  for (auto e : c->ev_hp)
+    if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return OF_OK;
