@@ -1138,7 +1138,12 @@ struct BigPhase {
 // OF_SOLVE_PRIO: a token-holding solve runs on its lane's high-priority
 // stream, so its blocks are dispatched ahead of other lanes' kernels as CUs
 // free up (a 252-block k_cgs launch needs 74 KB of LDS per CU, which the
-// weighted median's 19 KB waves otherwise keep refilling)
+// weighted median's 19 KB waves otherwise keep refilling: in the default
+// bench's trace the first launch of a 1080p fine solve takes 92 us median but
+// 851 us at p90).  Measured with the side-by-side solves: 42.0-43.1 vs
+// 45.0-45.2 pairs/s (3 reps, profiles/r3ai_solve_prio_ab.log), as round 3's
+// single-slot version was (-10 %): starving the other lanes costs more than
+// the CG gains.  Off.
 #ifndef OF_SOLVE_PRIO
 #define OF_SOLVE_PRIO 0
 #endif
