@@ -732,7 +732,8 @@ void cheb_poly(int m, double a, double b, double *cB) {
 // rows instead of 39 + 19 (the band halo is recomputed once per band).
 // Measured (round 3, 2 x 2 reps): 1 slot x 504 blocks 38.9, 2 x 504 40.7,
 // 2 x 336 42.8, 2 x 252 44.4 (4 lanes: 45.3), 2 x 200 42.9, 3 x 168 45.0,
-// 4 x 128 42.6 pairs/s (profiles/r3y_token_slots_ab.log, r3z_ab.log)
+// 4 x 128 42.6 pairs/s (profiles/r3y_token_slots_ab.log, r3z_ab.log); 2 x 270
+// (15 bands) 42.2, 3 x 252 44.3 vs 44.8 (profiles/r3ak_ab.log)
 #ifndef CGS_LANES_BLOCKS
 #define CGS_LANES_BLOCKS 252
 #endif
