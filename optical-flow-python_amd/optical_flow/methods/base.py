@@ -196,10 +196,12 @@ class BaseOpticalFlow(ABC):
         qd, qsu, qsv = self._qua_penalties()
         P.rho_data = d
         P.qua_data = qd
-        for k in range(2):
-            if k < len(su):
-                P.rho_spatial_u[k], P.rho_spatial_v[k] = su[k], sv[k]
-                P.qua_spatial_u[k], P.qua_spatial_v[k] = qsu[k], qsv[k]
+        # default-pair slots; a general filter list may carry fewer penalties
+        # per component (each list guarded on its own length)
+        for k in range(min(2, len(su))):
+            P.rho_spatial_u[k], P.qua_spatial_u[k] = su[k], qsu[k]
+        for k in range(min(2, len(sv))):
+            P.rho_spatial_v[k], P.qua_spatial_v[k] = sv[k], qsv[k]
         if self._general_filters():
             F = P.filters
             F.general = 1

@@ -512,6 +512,80 @@ def gen_filters():
     save("filters.npz", **out)
 
 
+def _enc(v):
+    """JSON encoding of one attribute value (data only: numbers, strings,
+    arrays, RobustFunction as its .method / .sigma)."""
+    if isinstance(v, RobustFunction):
+        return {"__robust__": v.method, "sigma": [float(s) for s in np.atleast_1d(v.sigma)]}
+    if isinstance(v, np.ndarray):
+        return {"__ndarray__": v.astype(float).ravel().tolist(), "shape": list(v.shape)}
+    if isinstance(v, (list, tuple)):
+        return [_enc(x) for x in v]
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    if v is None or isinstance(v, (bool, int, float, str)):
+        return v
+    raise TypeError(f"cannot encode {type(v)}")
+
+
+# parse_input_parameter overrides (base.py:65-85): dict, flat list (odd
+# trailing key ignored), the 'lambda' alias, unknown keys, penalty objects
+BAG_OVERRIDES = {
+    "classic+nl-fast|dict": ("classic+nl-fast", {"lambda": 5.0, "solver": "pcg", "bogus_key": 1}),
+    "classic-c|flat": ("classic-c", ["lambda", 2.5, "pcg_rtol", 1e-4, "max_iters", 4, "dangling"]),
+    "hs|dict": ("hs", {"lambda": 20, "sigmaD2": 2.0, "mf_iter": 2, "solver": "sor"}),
+    "classic++|robust": ("classic++", {"rho_data": RobustFunction("charbonnier", 0.01),
+                                       "median_filter_size": None, "lambda_q": 2.0}),
+}
+
+
+def gen_bags():
+    """The reference's method objects as attribute bags (class name + every
+    instance attribute except the image slots and the conv-matrix cache) for
+    the 12 registry names and BAG_OVERRIDES, after parse_input_parameter —
+    the input of tools/reference_hook.py:of_params_from."""
+    import json
+    cases = {m: (m, None) for m in METHODS}
+    cases.update(BAG_OVERRIDES)
+    out = {}
+    for tag, (m, prm) in cases.items():
+        o = ref_cfg.load_of_method(m)
+        if prm is not None:
+            o.parse_input_parameter(prm)
+        attrs = {k: _enc(v) for k, v in vars(o).items() if k not in ("images", "_cached_conv_mats")}
+        out[tag] = {"method": m, "params": _enc(prm) if not isinstance(prm, dict) else
+                    {k: _enc(v) for k, v in prm.items()},
+                    "class": type(o).__name__, "attrs": attrs}
+    path = os.path.join(HERE, "ref_bags.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(f"wrote ref_bags.json ({os.path.getsize(path)/1024:.1f} KiB, {len(out)} bags)")
+
+
+def gen_chaos_synth():
+    """The reference's own sensitivity on e2e_synth (synth_pair(120, 160, 0)):
+    the chaotic (charbonnier / generalized-charbonnier GNC) methods rerun
+    with frame 1 perturbed by 1e-12 relative noise, three seeds, EPE to the
+    unperturbed run.  Calibrates tests/test_gpu_e2e.py::test_e2e_synthetic."""
+    im1, im2, gt = synthetic.synth_pair(120, 160, 0)
+    out = {}
+    for m in ("classic-c", "classic++", "classic+nl-fast"):
+        base = quiet(ref.estimate_flow, im1, im2, m)
+        out[m] = base
+        for s in range(3):
+            rng = np.random.default_rng(9000 + s)
+            im1p = im1 * (1.0 + 1e-12 * rng.standard_normal(im1.shape))
+            uv = quiet(ref.estimate_flow, im1p, im2, m)
+            e = np.sqrt(((uv - base) ** 2).sum(-1))
+            out[f"{m}:spread{s}:mean"] = np.array(e.mean())
+            out[f"{m}:spread{s}:median"] = np.array(np.median(e))
+            out[f"{m}:spread{s}:p99"] = np.array(np.percentile(e, 99))
+            print(f"  {m} seed {s}: mean {e.mean():.3e} median {np.median(e):.3e}")
+    save("chaos_synth.npz", **out)
+
+
 if __name__ == "__main__":
     jobs = sys.argv[1:] or ["unit", "e2e_small", "e2e_synth"]
     for j in jobs:

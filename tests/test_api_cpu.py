@@ -266,31 +266,6 @@ def test_solver_geometry_bounds():
         _native.solver_geometry(0, 10, "pcg")
 
 
-def test_reference_hook_param_handling():
-    """The reference-side binding of INTEGRATION.md §3 (tools/reference_hook.py):
-    params go through parse_input_parameter ('lambda' -> lambda_, unknown keys
-    ignored, dict or flat list; base.py:65-85) before to_params()."""
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    import reference_hook
-    from optical_flow import _abi
-    ope, P = reference_hook.params_for("classic+nl-fast", {"lambda": 3.0, "bogus_key": 1, "solver": "pcg"})
-    assert ope.lambda_ == 3.0 and P.lambda_ == 3.0 and not hasattr(ope, "bogus_key")
-    assert P.solver == _abi.SOLVER["pcg"]
-    ope, P = reference_hook.params_for("hs", ["lambda", 2.0, "max_warping_iters", 5])
-    assert P.lambda_ == 2.0 and P.max_warping_iters == 5
-    _, P0 = reference_hook.params_for("classic+nl-fast")
-    assert P0.lambda_ == load_default_lambda("classic+nl-fast")
-    with pytest.raises(ValueError):
-        reference_hook.params_for("no-such-method")
-    with pytest.raises(ValueError):
-        reference_hook.params_for("classic+nl-fast", {"solver": "lu"})
-
-
-def load_default_lambda(name):
-    from optical_flow.methods.config import load_of_method
-    return load_of_method(name).lambda_
-
-
 def test_estimate_flow_batch_rejects_mixed_channels():
     """Every frame of both lists is checked before the [:, :, :3] slice (a 1-
     or 2-channel frame would otherwise pass as 3 and be over-read); raised
