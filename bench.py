@@ -56,6 +56,9 @@ KERNEL_BYTES_PER_PX = {
     "wmf": 8 + 4 + 12 + 8,                 # uv, occ, Lab -> uv
     "rof_iters": 4 + 8 + 8,                # im, p -> p per channel, ROF_K iterations per launch
     "sor_sweep": 36 + 8 + 8,               # 7 coef + 2 rhs planes, x read + write (52 B/px/sweep)
+    # the pipelined SOR: one launch per solve, bytes counted per sweep done
+    # ("sor_pipe.active" = sweeps x level pixels)
+    "sor_pipe": 36 + 8 + 8,
 }
 # VALU issue peak (MI355X_MICROARCH.md: a wave issues one VALU instruction per
 # 2 cycles per SIMD; 256 CUs x 4 SIMDs at 2.4 GHz): wave-instructions / s
@@ -300,17 +303,18 @@ def inner_loop_of(ktimes, per_level):
         elif name == "sor_sweep":
             byt += KERNEL_BYTES_PER_PX["sor_sweep"] * rec["px"]
             ms += rec["ms_total"]
-        elif name == "pcg_iter":
+        elif name in ("pcg_iter", "sor_pipe"):
             ms += rec["ms_total"]
         elif name in INNER_TIME_ONLY:
             ms += rec["ms_total"]
-    act = ktimes.get("pcg_iter.active")
-    if act:
-        byt += KERNEL_BYTES_PER_PX["pcg_iter"] * act["px"]
+    for it in ("pcg_iter", "sor_pipe"):
+        act = ktimes.get(it + ".active")
+        if act:
+            byt += KERNEL_BYTES_PER_PX[it] * act["px"]
     if ms <= 0:
         return None
     ach = byt / (ms * 1e-3) / 1e9
-    fine = max((px for (n, px) in per_level if n in ("pcg_iter", "sor_sweep")), default=None)
+    fine = max((px for (n, px) in per_level if n in ("pcg_iter", "sor_sweep", "sor_pipe")), default=None)
     out = {"bytes_per_step": round(byt), "kernel_ms_per_step": round(ms, 3), "achieved": round(ach, 1),
            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
            "formula": "sum N*(48|44 + 56 + 24) per warp + 76*N*K_pcg | 52*N*K_sor; time of warp, assembly, update, "
@@ -319,8 +323,9 @@ def inner_loop_of(ktimes, per_level):
         b2 = sum(INNER_BYTES[n] * r["px"] for (n, px), r in per_level.items() if px == fine and n in INNER_BYTES)
         b2 += KERNEL_BYTES_PER_PX["pcg_iter"] * per_level.get(("pcg_iter.active", fine), {"px": 0})["px"]
         b2 += KERNEL_BYTES_PER_PX["sor_sweep"] * per_level.get(("sor_sweep", fine), {"px": 0})["px"]
+        b2 += KERNEL_BYTES_PER_PX["sor_pipe"] * per_level.get(("sor_pipe.active", fine), {"px": 0})["px"]
         m2 = sum(r["ms_total"] for (n, px), r in per_level.items() if px == fine and
-                 (n in INNER_BYTES or n in ("pcg_iter", "sor_sweep") or n in INNER_TIME_ONLY))
+                 (n in INNER_BYTES or n in ("pcg_iter", "sor_sweep", "sor_pipe") or n in INNER_TIME_ONLY))
         if m2 > 0:
             a2 = b2 / (m2 * 1e-3) / 1e9
             out["finest"] = {"px": fine, "achieved": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4)}

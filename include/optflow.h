@@ -165,6 +165,13 @@ int of_synchronize(of_ctx *ctx);
  * name, 2 = keyed by "name@pixels" (one entry per kernel and level size);
  * see of_kernel_times */
 int of_set_profiling(of_ctx *ctx, int enable);
+/* solver options of a context (inherited by its batch lanes):
+ *   OF_OPT_SOR_PIPELINE  1 (default): 'sor' runs its sweeps pipelined in one
+ *                        persistent launch (k_sor_pipe); 0: one launch per
+ *                        sweep (k_sor_lex).  Both give the same iterate and
+ *                        sweep count bitwise. */
+#define OF_OPT_SOR_PIPELINE 1
+int of_set_option(of_ctx *ctx, int option, int value);
 /* kernel timing accumulated since enable: per kernel name total ms, launch
  * count and pixels processed (sum over launches of the level's H*W; ROF
  * counts H*W*channels); any output pointer may be NULL */

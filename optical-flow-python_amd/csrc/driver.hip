@@ -157,6 +157,12 @@ struct HostStage {
 // dynamic LDS of a k_sor_lex block: unused, it keeps one block per CU (the
 // measured configuration of the sc1 hand-off, MI355X_MICROARCH.md)
 #define OF_SOR_SHM (96 * 1024)
+// k_sor_pipe: persistent grid of one wave per CU; sync words (ticket, fail,
+// stop, counters, decisions, progress stamps) then per-strip partials and the
+// decided sweeps' sums
+#define OF_SOR_PIPE_WAVES 256
+#define OF_SORP_SYNC_BYTES (1024 + SOR_RING_MAX * 2 * SOR_MAXS * sizeof(int))
+#define OF_SORP_BYTES (OF_SORP_SYNC_BYTES + (SOR_RING_MAX * 2 * SOR_MAXS * 2 + SOR_RING_MAX * 2) * sizeof(double))
 
 struct of_ctx {
   int device = 0;
@@ -183,6 +189,8 @@ struct of_ctx {
   std::vector<PendingSolve> pend;
   double *d_partials = nullptr;
   unsigned *d_sor_sync = nullptr;
+  char *d_sorp = nullptr;  // k_sor_pipe sync words, partials (lazily allocated)
+  int opt_sor_pipe = 1;    // of_set_option(OF_OPT_SOR_PIPELINE)
   // solve log (of_set_solve_log): fp64 true residual of every solve
   int slog = 0;
   struct SolveLog {
@@ -932,8 +940,10 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     HIPCHK(hipMemcpyAsync(&c->h_ring[slot], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     return res;
   }
-  // lexicographic SOR (base.py:138-172): one launch per sweep, 64-row strips
-  // of the u half then of the v half (kernels_solve.hip, k_sor_lex)
+  // lexicographic SOR (base.py:138-172): 64-row strips of the u half then of
+  // the v half (kernels_solve.hip); k_sor_pipe runs many sweeps in flight in
+  // one persistent launch, k_sor_lex one launch per sweep (of_set_option
+  // OF_OPT_SOR_PIPELINE 0; the same iterate bitwise)
   REQUIRE(solver == OF_SOLVER_SOR, OF_EINVAL, "Unknown solver");
   const int nstrips = (H + 63) / 64;
   REQUIRE(nstrips <= SOR_MAXS, OF_ENOTSUP, "level too tall for the SOR kernel");
@@ -958,6 +968,52 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
   a.maxiter = P->sor_max_iters;
   HIPCHK(hipMemsetAsync(c->d_sor_sync, 0, OF_SOR_SYNC_BYTES, c->stream));
   launch(c, "sor_init", k_sor_init, dim3(std::min(1024, (H * b.P + 63) / 64)), dim3(64), 0, a);
+  if (c->opt_sor_pipe && a.maxiter > 0) {
+    // ring of S sweep buffers: enough for the sweeps the persistent grid (one
+    // wave per CU) can hold in flight, 2 * nstrips units per sweep
+    const int S = std::max(4, std::min(SOR_RING_MAX, OF_SOR_PIPE_WAVES / (2 * nstrips) + 2));
+    if (!c->d_sorp) HIPCHK(hipMalloc(&c->d_sorp, OF_SORP_BYTES));
+    SorPipeArgs q;
+    memset(&q, 0, sizeof(q));
+    q.coef = coef.p;
+    q.b = b.p;
+    q.x0 = x.p;
+    q.bstride = (size_t)H * b.P;
+    q.ring = (float2 *)c->arena.alloc(sizeof(float2) * q.bstride * S);
+    q.H = H;
+    q.W = W;
+    q.P = b.P;
+    q.ps = ps;
+    q.nstrips = nstrips;
+    q.S = S;
+    q.stride = W + 64;
+    char *z = c->d_sorp;
+    q.ticket = (unsigned *)z;
+    q.fail = (int *)(z + 64);
+    q.stop = (int *)(z + 128);
+    q.cnt = (int *)(z + 256);
+    q.dec = (int *)(z + 512);
+    q.prog = (int *)(z + 1024);
+    q.part = (double *)(z + OF_SORP_SYNC_BYTES);
+    q.res = q.part + (size_t)SOR_RING_MAX * 2 * SOR_MAXS * 2;
+    q.omega = (float)P->sor_omega;
+    q.tol = P->sor_tol;
+    q.maxiter = P->sor_max_iters;
+    HIPCHK(hipMemsetAsync(z, 0, OF_SORP_SYNC_BYTES, c->stream));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)q.stop, 0x7fffffff, 1, c->stream));
+    const int nwaves = (int)std::min<int64_t>(OF_SOR_PIPE_WAVES, (int64_t)a.maxiter * 2 * nstrips);
+    launch(c, "sor_pipe", k_sor_pipe, dim3(nwaves), dim3(64), OF_SOR_SHM, q);
+    Grid2 g = grid2(H, W);
+    launch(c, "sor_final", k_sor_pipe_final, g.grid, g.block, 0, q, x.p, c->d_state);
+    HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_norm, q.fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    REQUIRE(*(const int *)c->h_norm == 0, OF_EHIP, "SOR sweep hand-off timed out");
+    const PcgState &st = c->h_state[0];
+    REQUIRE(st.done != 0, OF_EHIP, "SOR pipeline ended without a decided sweep");
+    note_active(c, "sor_pipe", st.iter, (double)H * W);
+    return {st.iter, st.done, st.xnorm2 > 0 ? std::sqrt(st.rr / st.xnorm2) : 0.0};
+  }
   double *sor_part = c->d_partials + 10 * PCG_MAX_BLOCKS;  // 2 x [2 * nstrips][2]
   auto args_k = [&](int k) {
     SorArgs ak = a;
@@ -1728,6 +1784,7 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipMalloc(&c->d_rpart, sizeof(double) * 2 * PCG_MAX_BLOCKS));
     HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 4 * OF_SLOG_MAX));
     HIPCHK(hipFuncSetAttribute((const void *)k_sor_lex, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
+    HIPCHK(hipFuncSetAttribute((const void *)k_sor_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
     HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));
@@ -1764,6 +1821,7 @@ int of_ctx_destroy(of_ctx *c) {
   if (c->h_ring) hipHostFree(c->h_ring);
   hipFree(c->d_partials);
   hipFree(c->d_sor_sync);
+  if (c->d_sorp) hipFree(c->d_sorp);
   hipFree(c->d_rpart);
   hipFree(c->d_rlog);
   hipFree(c->d_mm);
@@ -1785,6 +1843,18 @@ const char *of_last_error(of_ctx *c) { return c ? c->err.c_str() : g_err.c_str()
 int of_synchronize(of_ctx *c) {
   if (!c) return OF_EINVAL;
   return hipStreamSynchronize(c->stream) == hipSuccess ? OF_OK : OF_EHIP;
+}
+
+int of_set_option(of_ctx *c, int option, int value) {
+  if (!c) return OF_EINVAL;
+  switch (option) {
+    case OF_OPT_SOR_PIPELINE:
+      c->opt_sor_pipe = value ? 1 : 0;
+      return OF_OK;
+    default:
+      c->err = "unknown option";
+      return OF_EINVAL;
+  }
 }
 
 int of_set_profiling(of_ctx *c, int enable) {
@@ -2031,6 +2101,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
     for (int li = 0; li < lanes; ++li) {
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
+      l->opt_sor_pipe = c->opt_sor_pipe;
       l->big = big_px > 0 ? &c->big_own : nullptr;
       l->big_px = big_px;
       th.emplace_back([c, l, li, lanes, nslots, P, st, &errs] {
@@ -2258,6 +2329,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
     for (int li = 0; li < lanes; ++li) {
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
+      l->opt_sor_pipe = c->opt_sor_pipe;
       l->big = OF_BIG_PX > 0 ? &c->big_own : nullptr;
       l->big_px = OF_BIG_PX;
       th.emplace_back([=, &errs] {

@@ -921,37 +921,42 @@ template __global__ void k_cg_small<0, false>(CgSmallArgs);
 template <int DEG, bool BLOCK>
 __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
   __shared__ float2 ex[2][CG_REG_PX];
+  // (u, v) weights of the edges right of / below every pixel: the left / up
+  // weights of pixel e are those of e - 1 / e - W (registers held all four
+  // and spilled 100 B/lane at 256 VGPRs)
+  __shared__ float2 w_rt[CG_REG_PX], w_dn[CG_REG_PX];
   __shared__ double red[2][CGR_T / 64][2];
   const int tid = threadIdx.x + threadIdx.y * CGS_BX, wv = tid >> 6;
   const int H = g.H, W = g.W, P = g.P, N = H * W;
   const size_t ps = g.ps;
   const float *cf = g.coef;
-  int e[CGR_M], ir[CGR_M], jr[CGR_M];
-  bool ok[CGR_M];
-  size_t kk[CGR_M];
-  // coefficients: weights of the edges right / left / down / up (u, v),
-  // the 2x2 block (a, c, d) and its inverse (ia, ic, id)
-  float wr_u[CGR_M], wl_u[CGR_M], wd_u[CGR_M], wu_u[CGR_M], wr_v[CGR_M], wl_v[CGR_M], wd_v[CGR_M], wu_v[CGR_M];
+  int e[CGR_M];
+  bool ok[CGR_M], hl[CGR_M], hu[CGR_M];  // pixel owned; has a left / upper neighbour
+  // coefficients: weights of the edges right / down (u, v), the 2x2 block
+  // (a, c, d) and its inverse (ia, ic, id)
+  float wr_u[CGR_M], wd_u[CGR_M], wr_v[CGR_M], wd_v[CGR_M];
   float ca[CGR_M], cc[CGR_M], cd[CGR_M], ia[CGR_M], ic[CGR_M], id[CGR_M];
   float2 x[CGR_M], r[CGR_M], p[CGR_M];
+  // pitched offset of owned pixel m (a macro: lambdas taking the arrays by
+  // reference made them addressable and spilled them)
+#define CGR_KOF(m) ((size_t)((ok[m] ? e[m] : 0) / W) * P + ((ok[m] ? e[m] : 0) % W))
 #pragma unroll
   for (int m = 0; m < CGR_M; ++m) {
     e[m] = tid + CGR_T * m;
     ok[m] = e[m] < N;
     const int ee = ok[m] ? e[m] : 0;
-    ir[m] = ee / W;
-    jr[m] = ee - ir[m] * W;
-    kk[m] = (size_t)ir[m] * P + jr[m];
-    const size_t k = kk[m];
-    const int i = ir[m], j = jr[m];
+    const int i = ee / W, j = ee - i * W;
+    const size_t k = (size_t)i * P + j;
+    hl[m] = ok[m] && j > 0;
+    hu[m] = ok[m] && i > 0;
     wr_u[m] = ok[m] && j + 1 < W ? cf[k] : 0.f;
-    wl_u[m] = ok[m] && j > 0 ? cf[k - 1] : 0.f;
     wd_u[m] = ok[m] && i + 1 < H ? cf[ps + k] : 0.f;
-    wu_u[m] = ok[m] && i > 0 ? cf[ps + k - P] : 0.f;
     wr_v[m] = ok[m] && j + 1 < W ? cf[2 * ps + k] : 0.f;
-    wl_v[m] = ok[m] && j > 0 ? cf[2 * ps + k - 1] : 0.f;
     wd_v[m] = ok[m] && i + 1 < H ? cf[3 * ps + k] : 0.f;
-    wu_v[m] = ok[m] && i > 0 ? cf[3 * ps + k - P] : 0.f;
+    if (ok[m]) {
+      w_rt[ee] = make_float2(wr_u[m], wr_v[m]);
+      w_dn[ee] = make_float2(wd_u[m], wd_v[m]);
+    }
     ca[m] = ok[m] ? cf[4 * ps + k] : 0.f;
     cc[m] = ok[m] ? cf[5 * ps + k] : 0.f;
     cd[m] = ok[m] ? cf[6 * ps + k] : 0.f;
@@ -964,7 +969,11 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
     r[m] = ok[m] ? g.b[k] : make_float2(0.f, 0.f);
     p[m] = make_float2(0.f, 0.f);
   }
+  __syncthreads();  // w_rt / w_dn complete
   int buf = 0, rb = 0;
+  // left / up weights of owned pixel m (0 without that neighbour)
+#define CGR_WL(m) (hl[m] ? w_rt[e[m] - 1] : make_float2(0.f, 0.f))
+#define CGR_WU(m) (hu[m] ? w_dn[e[m] - W] : make_float2(0.f, 0.f))
   // neighbour sum N f of owned pixel m after exch(f)
   // (macro, not a lambda taking the array: an array reference kept the
   // Horner temporaries addressable and spilled them to scratch)
@@ -974,14 +983,21 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
       if (ok[m]) ex[buf][e[m]] = (f)[m];              \
     __syncthreads();                                  \
   }
-  auto nsum = [&](int m) {
-    const float2 *X = ex[buf];
-    const int c = ok[m] ? e[m] : 0;
-    const float2 L = X[max(c - 1, 0)], R = X[min(c + 1, N - 1)], U = X[max(c - W, 0)], D = X[min(c + W, N - 1)];
-    return make_float2(wl_u[m] * L.x + wr_u[m] * R.x + wu_u[m] * U.x + wd_u[m] * D.x,
-                       wl_v[m] * L.y + wr_v[m] * R.y + wu_v[m] * U.y + wd_v[m] * D.y);
-  };
-  auto minv = [&](int m, float2 f) { return make_float2(ia[m] * f.x + ic[m] * f.y, ic[m] * f.x + id[m] * f.y); };
+#define nsum(m)                                                                                              \
+  ({                                                                                                         \
+    const float2 *X_ = ex[buf];                                                                              \
+    const int c_ = ok[m] ? e[m] : 0;                                                                         \
+    const float2 L_ = X_[max(c_ - 1, 0)], R_ = X_[min(c_ + 1, N - 1)], U_ = X_[max(c_ - W, 0)],              \
+                 D_ = X_[min(c_ + W, N - 1)];                                                                \
+    const float2 a_ = CGR_WL(m), b_ = CGR_WU(m);                                                             \
+    make_float2(a_.x * L_.x + wr_u[m] * R_.x + b_.x * U_.x + wd_u[m] * D_.x,                                 \
+                a_.y * L_.y + wr_v[m] * R_.y + b_.y * U_.y + wd_v[m] * D_.y);                                \
+  })
+#define minv(m, f)                                                                                           \
+  ({                                                                                                         \
+    const float2 f_ = (f);                                                                                   \
+    make_float2(ia[m] * f_.x + ic[m] * f_.y, ic[m] * f_.x + id[m] * f_.y);                                   \
+  })
   // fixed-order fp64 sums of two per-thread values over the workgroup
   auto reduce2 = [&](double v0, double v1, double &s0, double &s1) {
     v0 = wave_sum(v0);
@@ -1019,16 +1035,17 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
         const float2 *X = ex[buf];
         const int c = ok[m] ? e[m] : 0;
         const float2 L = X[max(c - 1, 0)], R = X[min(c + 1, N - 1)], U = X[max(c - W, 0)], D = X[min(c + W, N - 1)];
-        const float2 bm = ok[m] ? g.b[kk[m]] : make_float2(0.f, 0.f);
+        const float2 bm = ok[m] ? g.b[CGR_KOF(m)] : make_float2(0.f, 0.f);
+        const float2 a = CGR_WL(m), b = CGR_WU(m);
         const double su = (double)bm.x - ((double)ca[m] * x[m].x + (double)cc[m] * x[m].y) +
-                          (double)wl_u[m] * L.x + (double)wr_u[m] * R.x + (double)wu_u[m] * U.x +
+                          (double)a.x * L.x + (double)wr_u[m] * R.x + (double)b.x * U.x +
                           (double)wd_u[m] * D.x;
         const double sv = (double)bm.y - ((double)cc[m] * x[m].x + (double)cd[m] * x[m].y) +
-                          (double)wl_v[m] * L.y + (double)wr_v[m] * R.y + (double)wu_v[m] * U.y +
+                          (double)a.y * L.y + (double)wr_v[m] * R.y + (double)b.y * U.y +
                           (double)wd_v[m] * D.y;
         r[m] = ok[m] ? make_float2((float)su, (float)sv) : make_float2(0.f, 0.f);
         acc0 += (double)r[m].x * r[m].x + (double)r[m].y * r[m].y;
-        if (ok[m]) g.xh[kk[m]] = x[m];  // x_hi (read back by k_cg_finalize)
+        if (ok[m]) g.xh[CGR_KOF(m)] = x[m];  // x_hi (read back by k_cg_finalize)
         x[m] = make_float2(0.f, 0.f);
       }
       buf ^= 1;
@@ -1101,7 +1118,7 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
 #pragma unroll
   for (int m = 0; m < CGR_M; ++m)
     if (ok[m]) {
-      g.x[kk[m]] = x[m];
+      g.x[CGR_KOF(m)] = x[m];
     }
   if (tid == 0) {
     g.st->iter = it;
@@ -1112,6 +1129,11 @@ __global__ __launch_bounds__(CGR_T) void k_cg_reg(CgSmallArgs g) {
     g.st->upd_k = upd;
   }
 #undef CGR_EXCH
+#undef nsum
+#undef minv
+#undef CGR_KOF
+#undef CGR_WL
+#undef CGR_WU
 }
 template __global__ void k_cg_reg<CG_DEG, true>(CgSmallArgs);
 template __global__ void k_cg_reg<0, false>(CgSmallArgs);
@@ -1897,6 +1919,275 @@ __global__ __launch_bounds__(64) void k_sor_final(SorArgs a, int k) {
   a.st->rr = dn;
   a.st->xnorm2 = xn;
   a.st->done = sqrt(dn) < a.tol * sqrt(xn) ? 1 : 2;
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined lexicographic SOR: many sweeps in flight in ONE persistent launch.
+//
+// k_sor_lex runs one sweep per launch, so sweep k+1 starts only when the last
+// strip of sweep k has ended, and a 480x640 sweep keeps 16 waves busy on a
+// 1024-SIMD chip.  But Gauss-Seidel in lexicographic order needs, at point
+// (i, j) of sweep k+1, only values sweep k has already produced there: the
+// old u, v at (i, j), (i, j+1), (i+1, j), which sweep k wrote when its own
+// wavefront passed.  So sweep k+1 can trail sweep k at a fixed distance, and
+// so on: sweeps k+1, k+2, ... run side by side, each a wavefront behind the
+// previous one.  Every point is still relaxed from exactly the operands of
+// the reference's order, so the iterate is bitwise the one of k_sor_lex.
+//
+// Sweep k writes buffer k mod S of a ring of S (its own "new" values) and
+// reads the previous sweep's values from buffer (k-1) mod S (sweep 0 from the
+// zero field x).  So x_k survives until sweep k+S, and the stopping test of
+// sweep k (which needs all of its strips) may be decided after later sweeps
+// have started: the first sweep that passes ||x_k - x_{k-1}|| < tol ||x_k||
+// sets *stop = k, later sweeps abandon their work, and k_sor_pipe_final
+// copies buffer k mod S into x.  A unit (k, half, strip) that would
+// overwrite buffer k mod S first waits for sweep k-S's decision.
+//
+// Units are taken from a ticket counter in dependency order (sweep, then u
+// strips, then v strips), by waves of a persistent grid (one wave per CU, the
+// configuration of the sc1 hand-off, MI355X_MICROARCH.md "hand-offs" row 1):
+// every wait is on a lower ticket, so the launch cannot deadlock.  A unit
+// waits (wave-uniform polls of progress stamps = sweep * stride + steps) for
+//   - strip s-1 of its own sweep and half (the relaxed row above),
+//   - (v half) the u strip of its own rows in its own sweep,
+//   - strip s of sweep k-1's v half (old u, v of its rows: the v strip runs
+//     behind the u strip, so this covers both) and strip s+1 of sweep k-1's
+//     same half (the old row below).
+// The stopping test sums the per-strip fp64 partials in the same fixed order
+// as k_sor_lex; the last unit of a sweep to finish (an atomic count) decides.
+// Every wait is bounded and also ends when *fail or an earlier *stop is seen,
+// so the grid always drains.
+#define SOR_RING_MAX 32
+struct SorPipeArgs {
+  const float *coef;  // 7 planes, plane stride ps
+  const float2 *b;
+  const float2 *x0;   // zero field: the "previous sweep" of sweep 0
+  float2 *ring;       // S buffers of H x P float2, stride bstride
+  size_t bstride;
+  int H, W, P;
+  size_t ps;
+  int nstrips, S, stride;
+  unsigned *ticket;
+  int *fail;
+  int *stop;          // first sweep whose test passed / hit maxiter (0x7fffffff until then)
+  int *cnt;           // [S] finished units per ring slot (monotone)
+  int *dec;           // [S] (sweep + 1) * 4 + done code, once decided
+  int *prog;          // [S][2][SOR_MAXS] progress stamps
+  double *part;       // [S][2 * SOR_MAXS][2] per-strip (dn, xn)
+  double *res;        // [S][2] the decided sweep's (dn, xn)
+  float omega;
+  double tol;
+  int maxiter;
+};
+
+__device__ __forceinline__ float sor_ld1(const float *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sor_ldd(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sor_std(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave-uniform wait until *p >= need; false when the unit must be abandoned
+// (a later poll of *stop shows an earlier sweep finished the solve, or *fail)
+__device__ __forceinline__ bool sorp_wait(const SorPipeArgs &a, const int *p, int need, int &known, int k) {
+  for (int n = 0; known < need; ++n) {
+    known = __builtin_amdgcn_readfirstlane(sor_poll(p));
+    if (known >= need) break;
+    if ((n & 31) == 31) {
+      const int st = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
+      const int fl = __builtin_amdgcn_readfirstlane(sor_poll(a.fail));
+      if (st < k || fl) return false;
+    }
+    if (n > (1 << 21)) {
+      if (threadIdx.x == 0) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// unit (k, PH, s): strip s of half PH in sweep k; false if abandoned.  The
+// relaxation below is k_sor_lex's, operand for operand.
+template <int PH>
+__device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, double &dn, double &xn) {
+  const int lane = threadIdx.x, H = a.H, W = a.W, P = a.P;
+  const int i0 = s * 64, i = i0 + lane;
+  const bool rowok = i < H;
+  const size_t ps = a.ps;
+  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
+  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
+  const size_t row = (size_t)(rowok ? i : 0) * P;
+  const bool has_up = s > 0, has_dn = i0 + 64 < H;
+  const size_t row_up = (size_t)(has_up ? i0 - 1 : 0) * P, row_dn = (size_t)(has_dn ? i0 + 64 : 0) * P;
+  const int nsteps = W + 63;
+  const int S = a.S, cur = k % S, prv = (k + S - 1) % S;
+  float2 *xc = a.ring + (size_t)cur * a.bstride;
+  const float2 *xp = k > 0 ? a.ring + (size_t)prv * a.bstride : a.x0;
+  const int base = k * a.stride, pbase = (k - 1) * a.stride;
+  int *pk = a.prog + cur * 2 * SOR_MAXS;
+  const int *pp = a.prog + prv * 2 * SOR_MAXS;
+  int *my = pk + PH * SOR_MAXS + s;
+  const int *pup = pk + PH * SOR_MAXS + (s > 0 ? s - 1 : 0);
+  const int *pu = pk + s;                                       // (k, u, s)
+  const int *pold = pp + SOR_MAXS + s;                          // (k-1, v, s)
+  const int *pdn = pp + PH * SOR_MAXS + (has_dn ? s + 1 : s);   // (k-1, PH, s+1)
+  int known_up = 0, known_u = 0, known_old = 0, known_dn = 0;
+  const float om = a.omega, om1 = 1.0f - a.omega;
+  bool alive = true;
+
+  float2 X[8], XU[8], XD[8];
+  float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
+  auto fetch = [&](int t) {  // column t + SOR_D - lane
+    const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
+    if (has_up && tp >= 0 && tp < W) alive = alive && sorp_wait(a, pup, base + tp + 64, known_up, k);
+    if (PH == 1 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pu, base + tp + 1, known_u, k);
+    if (k > 0 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pold, pbase + tp + 1, known_old, k);
+    if (k > 0 && has_dn && tp - 63 >= 0 && tp - 63 < W)
+      alive = alive && sorp_wait(a, pdn, pbase + tp - 62, known_dn, k);
+    const bool ok = rowok && jp >= 0 && jp < W;
+    const size_t o = row + (ok ? jp : 0);
+    if (PH == 0) X[q] = ok ? sor_ld(xp + o) : make_float2(0.f, 0.f);
+    else X[q] = ok ? make_float2(sor_ld1((const float *)(xc + o)), sor_ld1((const float *)(xp + o) + 1))
+                   : make_float2(0.f, 0.f);
+    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
+    WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
+    DG[q] = ok ? dgp[o] : 0.f;
+    CC[q] = ok ? ccp[o] : 0.f;
+    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
+    if (lane == 0) {
+      const bool u = has_up && jp >= 0 && jp < W;
+      XU[q] = u ? sor_ld(xc + row_up + jp) : make_float2(0.f, 0.f);
+      WYU[q] = u ? wyp[row_up + jp] : 0.f;
+    }
+    if (lane == 63) {
+      const bool d = has_dn && jp >= 0 && jp < W;
+      XD[q] = d ? sor_ld(xp + row_dn + jp) : make_float2(0.f, 0.f);
+    }
+  };
+#pragma unroll
+  for (int t = -SOR_D; t < 0; ++t) fetch(t);
+  if (!alive) return false;
+
+  int stop_seen = 0x7fffffff;
+  float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
+  for (int t0 = 0; t0 < nsteps; t0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u;
+      if (t >= nsteps) break;
+      fetch(t);
+      const int j = t - lane, q = t & 7, q1 = (t + 1) & 7;
+      const bool act = rowok && j >= 0 && j < W;
+      const float2 xo = X[q];
+      const float old = PH ? xo.y : xo.x, other = PH ? xo.x : xo.y;
+      const float right = PH ? X[q1].y : X[q1].x;
+      float down = sor_from_down(right);
+      if (lane == 63) down = PH ? XD[q].y : XD[q].x;
+      float up = sor_from_up(res), wu = sor_from_up(wy_prev);
+      if (lane == 0) {
+        up = PH ? XU[q].y : XU[q].x;
+        wu = WYU[q];
+      }
+      const float sgm = BB[q] + wx_prev * res + WX[q] * right + WY[q] * down + wu * up - CC[q] * other;
+      const float dg = DG[q];
+      float nw = fabsf(dg) < 1e-15f ? old : om1 * old + om * sgm / dg;
+      if (act) {
+        const size_t o = row + j;
+        sor_st(xc + o, PH ? make_float2(other, nw) : make_float2(nw, other));
+        const double dd = (double)nw - (double)old;
+        dn += dd * dd;
+        xn += (double)nw * nw;
+      } else {
+        nw = 0.f;
+      }
+      res = nw;
+      wx_prev = act ? WX[q] : 0.f;
+      wy_prev = act ? WY[q] : 0.f;
+      if (((t + 1) & (SOR_G - 1)) == 0 || t + 1 == nsteps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(my, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // *stop as read at the previous publication (its load had a whole
+        // publication interval to return): abandon a sweep past the answer
+        if (stop_seen < k || !alive) return false;
+        stop_seen = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
+      }
+    }
+  }
+  return alive;
+}
+
+__global__ __launch_bounds__(64) void k_sor_pipe(SorPipeArgs a) {
+  const int lane = threadIdx.x, n2 = 2 * a.nstrips;
+  for (;;) {
+    int tk = 0;
+    if (lane == 0) tk = (int)atomicAdd(a.ticket, 1u);
+    tk = __builtin_amdgcn_readfirstlane(__shfl(tk, 0, 64));
+    const int k = tk / n2, r = tk - k * n2;
+    if (k >= a.maxiter) return;
+    if (__builtin_amdgcn_readfirstlane(sor_poll(a.stop)) < k || __builtin_amdgcn_readfirstlane(sor_poll(a.fail)))
+      return;
+    const int cur = k % a.S;
+    if (k >= a.S) {
+      // ring slot `cur` still holds sweep k - S: wait for its decision; if it
+      // ended the solve, this and every later unit is void
+      int known = 0;
+      const int need = (k - a.S + 1) * 4;
+      if (!sorp_wait(a, a.dec + cur, need, known, k)) return;
+      if (known & 3) return;
+    }
+    const int ph = r >= a.nstrips ? 1 : 0, s = ph ? r - a.nstrips : r;
+    double dn = 0.0, xn = 0.0;
+    const bool ok = ph ? sorp_unit<1>(a, k, s, dn, xn) : sorp_unit<0>(a, k, s, dn, xn);
+    if (!ok) continue;  // abandoned: the next ticket sees *stop / *fail and ends the wave
+    dn = wave_sum(dn);
+    xn = wave_sum(xn);
+    if (lane == 0) {
+      double *pt = a.part + ((size_t)cur * 2 * SOR_MAXS + r) * 2;  // fixed slot per strip, as k_sor_lex
+      sor_std(pt, dn);
+      sor_std(pt + 1, xn);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int c = atomicAdd(a.cnt + cur, 1) + 1;
+      if (c == (k / a.S + 1) * n2) {
+        // the last unit of sweep k: its stopping test (k_sor_lex's prologue)
+        double sd = 0.0, sx = 0.0;
+        for (int b = 0; b < n2; ++b) {
+          const double *q = a.part + ((size_t)cur * 2 * SOR_MAXS + b) * 2;
+          sd += sor_ldd(q);
+          sx += sor_ldd(q + 1);
+        }
+        const int done = sqrt(sd) < a.tol * sqrt(sx) ? 1 : (k + 1 >= a.maxiter ? 2 : 0);
+        sor_std(a.res + 2 * cur, sd);
+        sor_std(a.res + 2 * cur + 1, sx);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.dec + cur, (k + 1) * 4 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done) atomicMin(a.stop, k);
+      }
+    }
+  }
+}
+
+// after k_sor_pipe: x <- the decided sweep's buffer; the state as k_sor_final
+// records it (iter = sweeps done, rr = ||dx||^2, xnorm2 = ||x||^2)
+__global__ __launch_bounds__(256) void k_sor_pipe_final(SorPipeArgs a, float2 *x, PcgState *st) {
+  const int K = *a.stop;
+  if (K == 0x7fffffff || *a.fail) return;
+  const int cur = K % a.S;
+  const float2 *src = a.ring + (size_t)cur * a.bstride;
+  OF_FOR_PIXELS(a.H, a.W) {
+    if (j >= a.W) continue;
+    const size_t o = (size_t)i * a.P + j;
+    x[o] = src[o];
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
+    st->iter = K + 1;
+    st->rr = a.res[2 * cur];
+    st->xnorm2 = a.res[2 * cur + 1];
+    st->done = a.dec[cur] & 3;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -19,6 +19,7 @@ PENALTY = {
     "const": 100,
 }
 MAX_LEVELS = 32
+OF_OPT_SOR_PIPELINE = 1  # of_set_option
 
 
 class OfPenalty(C.Structure):

@@ -33,6 +33,7 @@ _SIGS = {
     "of_last_error": ([_vp], C.c_char_p),
     "of_synchronize": ([_vp], C.c_int),
     "of_set_profiling": ([_vp, C.c_int], C.c_int),
+    "of_set_option": ([_vp, C.c_int, C.c_int], C.c_int),
     "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _dp, _ip], C.c_int),
     "of_estimate_flow": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, C.c_int, _fp, _fp,
                           C.POINTER(OfStats)], C.c_int),
@@ -126,6 +127,10 @@ class Context:
         if rc == OF_ENOTSUP:
             raise NotImplementedError(msg)
         raise NativeError(msg)
+
+    def set_option(self, option, value):
+        """of_set_option (include/optflow.h), e.g. OF_OPT_SOR_PIPELINE."""
+        self.check(self.lib.of_set_option(self.handle, int(option), int(value)))
 
     def set_solve_log(self, enable=True):
         """Log the fp64 true residual of every linear solve (of_set_solve_log)."""

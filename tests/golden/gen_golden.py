@@ -565,24 +565,38 @@ def gen_bags():
 
 
 def gen_chaos_synth():
-    """The reference's own sensitivity on e2e_synth (synth_pair(120, 160, 0)):
-    the chaotic (charbonnier / generalized-charbonnier GNC) methods rerun
-    with frame 1 perturbed by 1e-12 relative noise, three seeds, EPE to the
-    unperturbed run.  Calibrates tests/test_gpu_e2e.py::test_e2e_synthetic."""
+    """The reference's own sensitivity on e2e_synth (synth_pair(120, 160, 0)).
+    estimate_flow quantizes RGB to uint8 gray (interface.py:74-88), which
+    absorbs any tiny perturbation of the frames, so the perturbation is
+    applied to frame 1's gray image after that step, relative noise of 1e-12
+    and of 6e-8 (float32 rounding), three seeds each; the rest is
+    estimate_flow's own body (interface.py:41-71).  EPE to the unperturbed
+    run.  Calibrates tests/test_gpu_e2e.py::test_e2e_synthetic."""
     im1, im2, gt = synthetic.synth_pair(120, 160, 0)
     out = {}
     for m in ("classic-c", "classic++", "classic+nl-fast"):
-        base = quiet(ref.estimate_flow, im1, im2, m)
+        def run(eps, seed):
+            o = ref_cfg.load_of_method(m)
+            g1, g2 = ref_iface._rgb2gray(im1), ref_iface._rgb2gray(im2)
+            if eps:
+                g1 = g1 * (1.0 + eps * np.random.default_rng(seed).standard_normal(g1.shape))
+            o.images = np.stack([g1, g2], axis=2)
+            if o.color_images is not None:
+                lab = ref_iface._rgb2lab(im1)
+                for j in range(lab.shape[2]):
+                    lab[:, :, j] = ref_ip.scale_image(lab[:, :, j], 0, 255)
+                o.color_images = lab
+            return quiet(o.compute_flow, np.zeros(im1.shape[:2] + (2,)))
+        base = run(0.0, 0)
+        assert np.array_equal(base, quiet(ref.estimate_flow, im1, im2, m)), m
         out[m] = base
-        for s in range(3):
-            rng = np.random.default_rng(9000 + s)
-            im1p = im1 * (1.0 + 1e-12 * rng.standard_normal(im1.shape))
-            uv = quiet(ref.estimate_flow, im1p, im2, m)
-            e = np.sqrt(((uv - base) ** 2).sum(-1))
-            out[f"{m}:spread{s}:mean"] = np.array(e.mean())
-            out[f"{m}:spread{s}:median"] = np.array(np.median(e))
-            out[f"{m}:spread{s}:p99"] = np.array(np.percentile(e, 99))
-            print(f"  {m} seed {s}: mean {e.mean():.3e} median {np.median(e):.3e}")
+        for eps in (1e-12, 6e-8):
+            for s in range(3):
+                e = np.sqrt(((run(eps, 9000 + s) - base) ** 2).sum(-1))
+                out[f"{m}:eps{eps:g}:seed{s}:mean"] = np.array(e.mean())
+                out[f"{m}:eps{eps:g}:seed{s}:median"] = np.array(np.median(e))
+                out[f"{m}:eps{eps:g}:seed{s}:p99"] = np.array(np.percentile(e, 99))
+                print(f"  {m} eps {eps:g} seed {s}: mean {e.mean():.3e} median {np.median(e):.3e}")
     save("chaos_synth.npz", **out)
 
 

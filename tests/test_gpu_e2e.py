@@ -26,9 +26,16 @@ def _aepe(uv, gt):
 #  - nlfast (Classic+NL-fast): 2.9e-5 / 4.4e-6 on the crop, 1.8e-4 / 1.2e-5 on
 #    the synthetic pair (the weighted median amplifies single-pixel flips);
 #  - nl (Classic+NL, gnc 3 with the 0.5 blend): 2.9e-3 / 4.0e-4;
-#  - chaotic (classic-c*, classic++): the reference itself moves by
-#    4.7e-3 / 5.4e-3 px mean when its direct solve is perturbed by 1e-12
-#    (relative); measured 1.2e-2 / 6.5e-3 at most;
+#  - chaotic (classic-c*, classic++): charbonnier GNC amplifies last-bit
+#    differences.  On the crop the reference itself moves by 4.7e-3 / 5.4e-3
+#    px mean when its direct solve is perturbed by 1e-12 (relative).  On the
+#    synthetic pair (tests/golden/chaos_synth.npz: frame 1's gray image
+#    perturbed after the uint8 quantization, 3 seeds) the reference moves by
+#    1.3-1.4e-2 mean / 8.7-8.8e-3 median (classic-c) and 8.6-8.9e-3 / 4.1-4.6e-3
+#    (classic++) at 1e-12, and by 1.9-2.1e-2 / 1.2-1.4e-2 (classic-c) at 6e-8
+#    (float32 rounding); the GPU's classic-c sits at 2.0e-2 / 1.33e-2 (round
+#    3), i.e. at the reference's own float32-level spread, and
+#    test_e2e_synthetic gates it at 2x the reference's 1e-12 spread;
 #  - classic-c-a: the reference diverges (|uv| ~ 3.6e36); so must we.
 TOL = {"stable": (2e-5, 1e-5), "nlfast": (5e-4, 4e-5), "nl": (1e-2, 2e-3), "chaotic": (3e-2, 2e-2)}
 FAMILY = {"classic+nl-fast": "nlfast", "classic+nl": "nl", "classic+nl-full": "nl", "hs-brightness": "stable",
@@ -65,17 +72,31 @@ def test_e2e_gray_and_pcg(golden):
     assert epe_stats(uv, d["pcg:hs"])["mean"] < 3e-2
 
 
-@pytest.mark.parametrize("method", ["classic+nl-fast", "hs", "classic-c", "hs-brightness"])
+@pytest.mark.parametrize("method", ["classic+nl-fast", "hs", "classic-c", "hs-brightness", "classic++"])
 def test_e2e_synthetic(golden, method):
+    """synth_pair(120, 160, 0) end to end vs the reference.  Chaotic methods
+    are gated at 2x the reference's own spread under a 1e-12 relative
+    perturbation of its gray input (max over 3 seeds, chaos_synth.npz), the
+    others by TOL; the float32-level (6e-8) spread is printed beside."""
     import optical_flow
     d = golden("e2e_synth.npz")
+    ch = golden("chaos_synth.npz")
+    ref = d[method] if method in d else ch[method]
     uv = optical_flow.estimate_flow(d["im1"], d["im2"], method)
-    s = epe_stats(uv, d[method])
-    da = abs(_aepe(uv, d["gt"]) - _aepe(d[method], d["gt"]))
-    print(method, s, "dAEPE", da)
+    s = epe_stats(uv, ref)
+    da = abs(_aepe(uv, d["gt"]) - _aepe(ref, d["gt"]))
     fam = FAMILY[method]
-    mean_tol, med_tol = TOL[fam]
-    assert s["mean"] < mean_tol and s["median"] < med_tol, s
+    print(method, s, "dAEPE", da)
+    if method in ch:
+        spread = {eps: (max(float(ch[f"{method}:eps{eps}:seed{k}:mean"]) for k in range(3)),
+                        max(float(ch[f"{method}:eps{eps}:seed{k}:median"]) for k in range(3)))
+                  for eps in ("1e-12", "6e-08")}
+        print("  reference spread (mean, median): 1e-12", spread["1e-12"], " 6e-8", spread["6e-08"])
+    if fam == "chaotic":
+        mean_tol, med_tol = 2 * spread["1e-12"][0], 2 * spread["1e-12"][1]
+    else:
+        mean_tol, med_tol = TOL[fam]
+    assert s["mean"] < mean_tol and s["median"] < med_tol, (s, mean_tol, med_tol)
     assert da < (3e-3 if fam == "chaotic" else 1e-3)
 
 

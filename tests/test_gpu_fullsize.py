@@ -126,3 +126,27 @@ def test_fullsize_1080_default_solve_log():
     a_gpu = _aepe(uv, gt)
     print(f"AEPE gpu backslash {a_gpu:.6f}  ref pcg {float(d['aepe_gt']):.6f}")
     assert abs(a_gpu - float(d["aepe_gt"])) <= 1e-3  # measured 1.2e-5
+
+
+def test_fullsize_1080_timed_geometry():
+    """The path bench.py times: of_pairs_run_host on
+    uint8 1080p pairs with several lanes, where the fine CG solves of two
+    pairs run side by side at 252 blocks each.  Pair 0 is
+    synth_pair(1080, 1920, 0), compared with the reference's own default-solver
+    run (ref1080_backslash_sub4.npz) under the cfg4 gates; the other lanes'
+    pairs (seeds 1..3) keep the side-by-side token busy."""
+    import optical_flow
+    from optical_flow.utils.synthetic import synth_pair
+    d = dict(np.load(os.path.join(GOLDEN, "ref1080_backslash_sub4.npz")))
+    pairs = [synth_pair(1080, 1920, s) for s in range(4)]
+    a = [p[0].astype(np.uint8) for p in pairs]
+    b = [p[1].astype(np.uint8) for p in pairs]
+    flows = optical_flow.estimate_flow_batch(a, b, "classic+nl-fast", lanes=4)
+    uv, gt = flows[0], pairs[0][2]
+    assert np.all(np.isfinite(uv))
+    s = epe_stats(uv[::4, ::4], d["uv_sub4"].astype(np.float64))
+    a_gpu, a_ref = _aepe(uv, gt), float(d["aepe_gt"])
+    print(f"timed geometry: AEPE gpu {a_gpu:.6f} ref {a_ref:.6f} d {a_gpu - a_ref:+.2e}  EPE-to-ref {s}")
+    assert abs(a_gpu - a_ref) <= 1e-3
+    g_mean, g_med, g_p99 = CASES["cfg4_classic_nl_fast_1080"][-1]
+    assert s["mean"] <= g_mean and s["median"] <= g_med and s["p99"] <= g_p99, s

@@ -186,6 +186,53 @@ def test_sor_synthetic_vs_oracle(H, W):
     assert err <= 1e-4, err
 
 
+def _sor_both(fn):
+    """fn() with the pipelined SOR (k_sor_pipe, default) and with one launch
+    per sweep (k_sor_lex) on this thread's context."""
+    from optical_flow import _native as nat
+    from optical_flow._abi import OF_OPT_SOR_PIPELINE
+    ctx = nat.context()
+    try:
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 0)
+        ref = fn()
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
+        return fn(), ref
+    finally:
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
+
+
+@pytest.mark.parametrize("H,W,maxit", [(40, 56, 10000), (64, 64, 10000), (150, 200, 10000), (300, 90, 10000),
+                                       (520, 70, 10000), (130, 333, 7), (200, 131, 1)])
+def test_sor_pipelined_bitwise(H, W, maxit):
+    """k_sor_pipe (sweeps in flight side by side in one persistent launch)
+    gives the same iterate and sweep count bitwise as k_sor_lex (one launch
+    per sweep): every point is relaxed from the same operands.  Sizes cover
+    1..9 strips, the ring wrapping many times, and the sweep limit (done=2)."""
+    from optical_flow.methods.config import load_of_method
+    A, b = _spd_flow_system(H, W, seed=11 * H + W)
+    o = load_of_method("hs")
+    o.solver = "sor"
+    o.sor_max_iters = maxit
+
+    def run():
+        x = o._solve_linear_system(A, b, (H, W, 2))
+        return x, dict(o.last_solve)
+    (x1, s1), (x0, s0) = _sor_both(run)
+    assert s1["iters"] == s0["iters"] and s1.get("done") == s0.get("done"), (s1, s0)
+    if maxit < 10000:
+        assert s1["iters"] == maxit
+    np.testing.assert_array_equal(x1, x0)
+
+
+def test_sor_pipelined_bitwise_e2e(golden):
+    """HS with 'sor' end to end (every level, every warp) on the synthetic
+    pair: the pipelined and per-sweep kernels give bitwise the same flow."""
+    import optical_flow
+    d = golden("e2e_synth.npz")
+    uv1, uv0 = _sor_both(lambda: optical_flow.estimate_flow(d["im1"], d["im2"], "hs", {"solver": "sor"}))
+    np.testing.assert_array_equal(uv1, uv0)
+
+
 def test_occlusion(golden):
     from optical_flow.utils.occlusion import detect_occlusion
     d = golden("occlusion.npz")
