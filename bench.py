@@ -178,12 +178,21 @@ def cpu_baseline(args):
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
+WORKLOAD = None  # method@HxW/solver of this run (main)
+
+
+def workload_key(args):
+    return f"{args.method}@{args.height}x{args.width}/{args.solver or 'backslash'}"
+
+
 def load_pmc(kernel):
-    """The kernel's record in the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by tools/prof_summary.py --traffic
-    from tools/profile.sh's counter passes; shipped to the GPU box), or {}."""
+    """The kernel's record for THIS run's workload in the committed rocprofv3
+    PMC summary (profiles/pmc_traffic.json, keyed by workload then kernel,
+    written by tools/prof_summary.py --traffic from tools/profile.sh's counter
+    passes; shipped to the GPU box), or {} when that workload was not
+    profiled (then `traffic` is null rather than another kernel's figure)."""
     try:
-        return json.load(open(PMC_FILE)).get(kernel, {}) or {}
+        return (json.load(open(PMC_FILE)).get(WORKLOAD, {}) or {}).get(kernel, {}) or {}
     except (OSError, ValueError):
         return {}
 
@@ -193,6 +202,28 @@ def load_pmc_traffic(kernel, which="finest"):
     pmc_traffic.json): averaged over all launches ("all") or over the finest
     level's launches ("finest")."""
     return load_pmc(kernel).get("hbm_bytes_per_launch_all" if which == "all" else "hbm_bytes_per_launch")
+
+
+def pmc_symbol(kernel):
+    return load_pmc(kernel).get("symbol")
+
+
+# the reference's own run of each BASELINE.json config on synth_pair(H, W, 0)
+# (tests/golden/gen_golden.py full*): its AEPE against the analytic GT
+REF_FIXTURE = {"classic+nl-fast@1080x1920/backslash": "ref1080_backslash_sub4.npz",
+               "classic+nl-fast@1080x1920/pcg": "ref1080_pcg_sub4.npz",
+               "classic-c@720x1280/pcg": "ref720_classic_c_pcg_sub4.npz",
+               "hs@480x640/sor": "ref480_hs_sor_sub2.npz"}
+
+
+def ref_aepe():
+    f = REF_FIXTURE.get(WORKLOAD)
+    if not f:
+        return None, None
+    try:
+        return float(np.load(os.path.join(ROOT, "tests", "golden", f))["aepe_gt"]), f
+    except (OSError, KeyError, ValueError):
+        return None, f
 
 
 def wmf_compute_roofline(per_level):
@@ -256,11 +287,21 @@ def roofline_of(ktimes, per_level):
     return out
 
 
-def profiled_replay(ctx, lib, P0, pairs, lanes):
+def profiled_replay(ctx, lib, P0, pairs, lanes, timeline=None):
     """One step of of_pairs_run with per-launch HIP-event timing keyed by
-    kernel and level size; returns (per-kernel totals, per-(kernel, px))."""
-    ctx.check(lib.of_set_profiling(ctx.handle, 2))
+    kernel and level size; returns (per-kernel totals, per-(kernel, px)).
+    With a `timeline` list, every launch's (name, px, t0_ms, t1_ms) on the
+    lanes' common time axis is appended to it (profiling mode 3)."""
+    ctx.check(lib.of_set_profiling(ctx.handle, 3 if timeline is not None else 2))
     run_step(ctx, P0, pairs, lanes)
+    if timeline is not None:
+        m = C.c_int(0)
+        ctx.check(lib.of_kernel_timeline(ctx.handle, 0, None, None, None, None, C.byref(m)))
+        k = m.value
+        nm = (C.c_char_p * k)()
+        px, t0, t1 = (C.c_double * k)(), (C.c_double * k)(), (C.c_double * k)()
+        ctx.check(lib.of_kernel_timeline(ctx.handle, k, nm, px, t0, t1, C.byref(m)))
+        timeline.extend((nm[i].decode(), px[i], t0[i], t1[i]) for i in range(min(k, m.value)))
     n = C.c_int(0)
     names = (C.c_char_p * 1024)()
     ms = (C.c_double * 1024)()
@@ -332,6 +373,36 @@ def inner_loop_of(ktimes, per_level):
     return out
 
 
+def as_timed_of(timeline, per_level, dom, fine):
+    """The dominant kernel's finest-level launches AS TIMED (the lanes replay:
+    several pairs in flight, two fine CG solves side by side): algorithmic
+    bytes of their active launches / the UNION of their [start, end]
+    intervals on the common time axis, i.e. the aggregate rate while any of
+    them runs; `overlap` = share of that union with >= 2 of them running."""
+    iv = sorted((t0, t1) for (n, px, t0, t1) in timeline if n == dom and px == fine)
+    if not iv:
+        return None
+    ev = sorted([(a, 1) for a, _ in iv] + [(b, -1) for _, b in iv])
+    union = over = 0.0
+    depth, last = 0, ev[0][0]
+    for t, d in ev:
+        if depth >= 1:
+            union += t - last
+        if depth >= 2:
+            over += t - last
+        depth += d
+        last = t
+    act = per_level.get((dom + ".active", fine)) or per_level.get((dom, fine))
+    byt = KERNEL_BYTES_PER_PX[dom] * act["px"]
+    ach = byt / (union * 1e-3) / 1e9
+    return {"kernel": dom, "px_per_launch": int(fine), "launches": len(iv), "active_launches": act["launches"],
+            "union_ms": round(union, 3), "overlap": round(over / union, 3) if union > 0 else None,
+            "mean_launch_ms": round(sum(b - a for a, b in iv) / len(iv), 5), "achieved": round(ach, 1),
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "method": "lanes replay as timed; HIP events on each lane's stream; bytes of the active launches / "
+                      "union of the launches' intervals (tools/side_by_side_rocprof.py's method)"}
+
+
 def kms(kt, pairs, top=14):
     return {k: round(v["ms_total"] / pairs, 3) for k, v in
             sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])[:top] if not k.endswith(".active")}
@@ -345,6 +416,8 @@ def metric_name(args):
 
 def main():
     args = parse()
+    global WORKLOAD
+    WORKLOAD = workload_key(args)
     dist, world, rank, local = dist_setup(args)
     ctx = _native.Context(local)
     lib = ctx.lib
@@ -416,7 +489,11 @@ def main():
     uv = np.empty((2, H, W), dtype=np.float32)
     ctx.check(lib.of_pair_download(ctx.handle, 0, _native.ptr(uv)))
     uv = np.moveaxis(uv, 0, 2)
-    aepe = float(np.sqrt(((uv - gts[0]) ** 2).sum(-1)).mean())
+    aepe_single = float(np.sqrt(((uv - gts[0]) ** 2).sum(-1)).mean())
+    # the timed (host-to-host, lanes) flow of pair 0 = synth_pair(H, W, 0) on
+    # rank 0, against the analytic GT and against the reference's own AEPE
+    aepe = float(np.sqrt(((np.moveaxis(outs[0], 0, 2) - gts[0]) ** 2).sum(-1)).mean())
+    a_ref, ref_fix = ref_aepe()
     sd = st.as_dict()
 
     roofline = None
@@ -426,7 +503,8 @@ def main():
     if not args.no_profile:
         # profiled replay of one step, same pairs and lanes as the timed
         # steps: HIP events around every launch on the stream it runs on
-        ktimes, per_level = profiled_replay(ctx, lib, P0, args.pairs, args.lanes)
+        tline = []
+        ktimes, per_level = profiled_replay(ctx, lib, P0, args.pairs, args.lanes, timeline=tline)
         pcg_levels = [{"px": px, "ms": round(rec["ms_total"] / args.pairs, 3), "launches": rec["launches"] / args.pairs,
                        "active": per_level.get(("pcg_iter.active", px), {}).get("launches", 0) / args.pairs}
                       for (n, px), rec in sorted(per_level.items(), key=lambda kv: -kv[0][1]) if n == "pcg_iter"]
@@ -447,6 +525,11 @@ def main():
                 "inner_loop_frac": conc["frac"] if conc else None}
             roofline["inner_loop"] = inner
             roofline["wmf"] = wmf_compute_roofline(pl1)
+            roofline["symbol"] = pmc_symbol(roofline["kernel"])
+            roofline["pmc_workload"] = WORKLOAD if load_pmc(roofline["kernel"]) else None
+            lv = [px for (n, px) in per_level if n == roofline["kernel"]]
+            if lv:
+                roofline["as_timed"] = as_timed_of(tline, per_level, roofline["kernel"], max(lv))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -471,7 +554,13 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
             "ms_per_level": [{"stage": l["stage"], "h": l["h"], "w": l["w"], "ms": round(l["ms"], 3)}
                              for l in sd["levels"]],
-            "aepe_gt": round(aepe, 5), "solver_iters_total": sd["solver_iters_total"],
+            "aepe_gt": round(aepe, 6),
+            "aepe_ref": None if a_ref is None or seeds[0] != 0 else {
+                "ref_aepe_gt": round(a_ref, 6), "aepe_ref_delta": round(aepe - a_ref, 7),
+                "fixture": f"tests/golden/{ref_fix}",
+                "note": "timed flow of synth_pair(H, W, 0) vs the reference's own estimate_flow on the same pair"},
+            "aepe_gt_single_pair": round(aepe_single, 6),
+            "solver_iters_total": sd["solver_iters_total"],
             "solver_iters_max": sd["solver_iters_max"], "solves": sd["solves"],
             "pcg_per_level": pcg_levels,
             # HIP-event kernel time per pair: isolated = the lanes=1 replay

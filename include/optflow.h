@@ -163,7 +163,8 @@ const char *of_last_error(of_ctx *ctx);
 int of_synchronize(of_ctx *ctx);
 /* per-kernel HIP-event timing on the ctx stream: 0 = off, 1 = keyed by kernel
  * name, 2 = keyed by "name@pixels" (one entry per kernel and level size);
- * see of_kernel_times */
+ * 3 = as 2, and every launch's start / end is also kept on a common time
+ * axis across the batch lanes (of_kernel_timeline); see of_kernel_times */
 int of_set_profiling(of_ctx *ctx, int enable);
 /* solver options of a context (inherited by its batch lanes):
  *   OF_OPT_SOR_PIPELINE  1 (default): 'sor' runs its sweeps pipelined in one
@@ -176,6 +177,11 @@ int of_set_option(of_ctx *ctx, int option, int value);
  * count and pixels processed (sum over launches of the level's H*W; ROF
  * counts H*W*channels); any output pointer may be NULL */
 int of_kernel_times(of_ctx *ctx, int max, const char **names, double *ms, int64_t *count, double *pixels, int *n);
+/* profiling mode 3: launches since enable, each with its kernel name, level
+ * pixels and [start, end] in ms after the enable call (HIP events; lanes of a
+ * batch share the time axis); *n = number of launches recorded */
+int of_kernel_timeline(of_ctx *ctx, int max, const char **names, double *pixels, double *t0_ms, double *t1_ms,
+                       int *n);
 
 /*
  * Whole pair: estimate_flow (optical_flow/interface.py:11-71) without its
@@ -220,8 +226,12 @@ int of_pair_run(of_ctx *ctx, int slot, of_params *params, of_stats *stats);
 /* run estimate_flow on slots 0..nslots-1 with `lanes` concurrent pipelines
  * (1..16; each its own HIP stream, device arena and solver state, driven by
  * its own host thread; slot s runs on lane s % lanes).  params is copied per
- * slot and not written back; stats (may be NULL) receives slot 0's.  Results
- * are bitwise independent of `lanes`.  Returns when every slot is done. */
+ * slot and not written back; stats (may be NULL) receives slot 0's.  Returns
+ * when every slot is done.  Results: lanes == 1 is bitwise estimate_flow;
+ * lanes >= 2 are bitwise equal to each other, and equal to estimate_flow for
+ * pairs below 2^20 px; at >= 2^20 px their fine CG solves run two pairs side
+ * by side in a different block geometry, so they differ from estimate_flow
+ * by CG rounding only (both meet the 1e-6 true residual). */
 int of_pairs_run(of_ctx *ctx, int nslots, const of_params *params, int lanes, of_stats *stats);
 /* host-to-host batch (the SURVEY.md §8d headline; replaces a Python loop of
  * estimate_flow(im1[k], im2[k], method) calls, interface.py:11-71): reads
@@ -233,9 +243,30 @@ int of_pairs_run(of_ctx *ctx, int nslots, const of_params *params, int lanes, of
  * slots 0..npairs-1 (of_pair_download, of_rccl_gather_flows); frames an
  * earlier of_pair_upload left in those slots are released (re-upload before
  * of_pair_run / of_pairs_run).  Results equal of_pairs_run on the same frames
- * (bitwise, independent of `lanes`). */
+ * with the same `lanes` (bitwise; see of_pairs_run for the lanes contract). */
 int of_pairs_run_host(of_ctx *ctx, int npairs, const uint8_t *const *im1, const uint8_t *const *im2, int H, int W,
                       int C, const of_params *params, int lanes, float *const *out_uv, of_stats *stats);
+/*
+ * Streaming host-to-host batch (the reference's per-pair loop over files,
+ * flo_io.py:46-113 / metrics.py:5-53, with host I/O overlapped): a pool of
+ * `lanes` pipelines (child contexts, one host thread each; lanes >= 2 share
+ * the fine-solve token as of_pairs_run) takes (H, W, C) uint8 pairs from a
+ * queue, so the lanes never drain between the caller's submissions.
+ *   of_pairs_open   start the pool for one frame shape and parameter set
+ *   of_pairs_submit queue n pairs; returns at once; the caller keeps im1[k],
+ *                   im2[k] and out_uv[k] (planar 2 x H x W fp32) alive until
+ *                   the pair is waited for; *first_ticket (may be NULL)
+ *                   receives the first pair's ticket, the others follow
+ *   of_pairs_wait   block until that pair's flow is in its out_uv
+ *   of_pairs_close  finish the queued pairs, stop and free the pool
+ * Flows equal of_pairs_run_host's with the same `lanes` bitwise.  While a
+ * stream is open, of_pairs_run / of_pairs_run_host refuse the context.
+ */
+int of_pairs_open(of_ctx *ctx, int H, int W, int C, const of_params *params, int lanes);
+int of_pairs_submit(of_ctx *ctx, int n, const uint8_t *const *im1, const uint8_t *const *im2, float *const *out_uv,
+                    int64_t *first_ticket);
+int of_pairs_wait(of_ctx *ctx, int64_t ticket);
+int of_pairs_close(of_ctx *ctx);
 /* D2H of a slot's flow (planar 2 x H x W) */
 int of_pair_download(of_ctx *ctx, int slot, float *out_uv);
 

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -134,9 +135,12 @@ struct Slot {
 // two device frame buffers, so pair j+1's bytes go up on the copy stream and
 // pair j-1's flow comes down while pair j computes.  All lanes share the
 // parent context's copy stream (`copy`, owned when own_copy): lanes + 1
-// streams in all, within GPU_MAX_HW_QUEUES (4) for lanes <= 3.  No copy waits
-// on a lane's kernels inside the stream (the helper threads wait on the host),
-// so one lane's copies never queue behind another lane's pair.
+// streams in all.  That fits GPU_MAX_HW_QUEUES (4) for lanes <= 3; the
+// default 4 lanes oversubscribe it (5 streams, so two share a hardware queue
+// and that lane's kernels and the copies queue behind each other), which was
+// measured as a net gain all the same: 45.3 vs 44.4 pairs/s at 3 lanes
+// (profiles/r3z_ab.log).  No copy waits on a lane's kernels inside the copy
+// stream (the helper threads wait on the host).
 struct HostStage {
   hipStream_t copy = nullptr;
   bool own_copy = false;
@@ -210,10 +214,20 @@ struct of_ctx {
   size_t tev_used = 0;
   std::vector<ProfRec> pending;
   std::map<std::string, KTime> ktimes;
+  // profiling mode 3: every launch's [start, end] in ms after `epoch` (an
+  // event on the parent context's stream; lanes share it)
+  struct TlRec {
+    const char *name;
+    double px, t0, t1;
+  };
+  std::vector<TlRec> tl;
+  hipEvent_t epoch = nullptr;
+  bool own_epoch = false;
   std::map<int64_t, int> iter_hints;  // (H, W, solver) -> last iteration count
   double cur_px = 0;  // pixels processed by the launches being issued (profiling)
   std::vector<Slot> slots;
   HostStage *hs = nullptr;      // of_pairs_run_host staging (lazily created)
+  struct PairPool *pool = nullptr;  // of_pairs_open streaming batch (lanes of its own)
   std::vector<of_ctx *> lanes;  // of_pairs_run pipelines: own stream, arena and solver state
   Token big_own;                // (parent) the big-phase token its lanes share
   Token *big = nullptr;         // (lane) token held through phases of >= big_px pixels
@@ -248,11 +262,17 @@ void flush_prof(of_ctx *c) {
   for (auto &r : c->pending) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
-    auto &s = c->prof == 2 ? c->ktimes[std::string(r.name) + "@" + std::to_string((long long)r.px)]
+    auto &s = c->prof >= 2 ? c->ktimes[std::string(r.name) + "@" + std::to_string((long long)r.px)]
                            : c->ktimes[r.name];
     s.ms += ms;
     s.px += r.px;
     s.n += 1;
+    if (c->prof == 3 && c->epoch) {
+      float a = 0, b = 0;
+      HIPCHK(hipEventElapsedTime(&a, c->epoch, r.e0));
+      HIPCHK(hipEventElapsedTime(&b, c->epoch, r.e1));
+      c->tl.push_back({r.name, r.px, a, b});
+    }
   }
   c->pending.clear();
   c->ev_used = 0;
@@ -666,7 +686,7 @@ int& iter_hint(of_ctx *c, int H, int W, int solver) {
 void note_active(of_ctx *c, const char *name, int launches, double px) {
   if (!c->prof) return;
   const std::string key = std::string(name) + ".active";
-  auto &s = c->ktimes[c->prof == 2 ? key + "@" + std::to_string((long long)px) : key];
+  auto &s = c->ktimes[c->prof >= 2 ? key + "@" + std::to_string((long long)px) : key];
   s.px += launches * px;
   s.n += launches;
 }
@@ -1389,6 +1409,37 @@ SolveResult gen_solve(of_ctx *c, const of_params *P, const GenLevel &L, const F2
   return {iters, rel <= P->exact_rtol ? 1 : done, rel};
 }
 
+// gen_solve with the solve log (of_set_solve_log): the fp64 true residual
+// ||b - A x|| / ||b|| of the DIA operator (k_dia_resid) for the iterate and
+// the returned x (the same fp32 field here)
+SolveResult gen_solve_logged(of_ctx *c, const of_params *P, const GenLevel &L, const F2 &b, const F2 &x) {
+  const SolveResult r = gen_solve(c, P, L, b, x);
+  if (c->slog && c->slog_rec.size() < OF_SLOG_MAX) {
+    const int idx = (int)c->slog_rec.size();
+    double *out = c->d_rlog + 4 * idx;
+    DiaArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pl = L.pl.p;
+    a.ps = L.pl.ps();
+    a.D = L.D;
+    a.H = b.H;
+    a.W = b.W;
+    a.P = b.P;
+    a.b = b.p;
+    a.x = x.p;
+    a.part = c->d_partials;
+    Grid2 g = grid2(b.H, b.W, PCG_MAX_BLOCKS);
+    launch(c, "dia_resid", k_dia_resid, g.grid, g.block, 0, a, L.t.p);
+    launch(c, "dia_sum", k_dia_sum, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)(c->d_partials + 8 * PCG_MAX_BLOCKS),
+           g.nblocks, out);
+    launch(c, "norm2", k_norm2_part, g.grid, g.block, 0, (const float2 *)b.p, b.H, b.W, b.P, c->d_rpart);
+    launch(c, "norm2", k_norm2_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_rpart, g.nblocks, out + 1);
+    HIPCHK(hipMemcpyAsync(out + 2, out, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    c->slog_rec.push_back({b.H, b.W, P->solver, -1, r.iters, r.done, r.rel});
+  }
+  return r;
+}
+
 // HSOpticalFlow.compute_flow_base (hs.py:109-142)
 void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
@@ -1438,7 +1489,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
     for (int jl = 0; jl < max_linear; ++jl) {
       if (gen) {
         gen_flow_operator(c, P, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, GL, rhs);
-        note_solve(c, st, gen_solve(c, P, GL, rhs, x));
+        note_solve(c, st, gen_solve_logged(c, P, GL, rhs, x));
       } else {
         flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
         note_solve(c, st, solve_tok(c, P, coef, rhs, x));
@@ -1497,7 +1548,7 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
     for (int jl = 0; jl < P->max_linear; ++jl) {
       if (gen) {
         gen_flow_operator(c, P, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, GL, rhs);
-        note_solve(c, st, gen_solve(c, P, GL, rhs, x));
+        note_solve(c, st, gen_solve_logged(c, P, GL, rhs, x));
       } else {
         flow_operator(c, o, uv, have_duv ? &duv : nullptr, It, Ix, Iy, &uvhat, coef, rhs);
         note_solve(c, st, solve_tok(c, P, coef, rhs, x));
@@ -1799,6 +1850,7 @@ int of_ctx_create(int device, of_ctx **out) {
 
 int of_ctx_destroy(of_ctx *c) {
   if (!c) return OF_OK;
+  if (c->pool) of_pairs_close(c);
   for (of_ctx *l : c->lanes) of_ctx_destroy(l);
   c->lanes.clear();
   hipSetDevice(c->device);
@@ -1811,6 +1863,7 @@ int of_ctx_destroy(of_ctx *c) {
     hipFree(s.rgb2);
     hipFree(s.uv);
   }
+  if (c->own_epoch && c->epoch) hipEventDestroy(c->epoch);
   for (auto e : c->ev_pool) hipEventDestroy(e);
   for (auto e : c->tev_pool) hipEventDestroy(e);
   for (auto e : c->ev_state)
@@ -1864,8 +1917,18 @@ int of_set_profiling(of_ctx *c, int enable) {
   } catch (const OfError &e) {
     return fail(c, e);
   }
-  c->prof = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
-  if (enable) c->ktimes.clear();
+  c->prof = enable < 0 ? 0 : (enable > 3 ? 3 : enable);
+  if (enable) {
+    c->ktimes.clear();
+    c->tl.clear();
+  }
+  if (c->prof == 3) {
+    if (!c->epoch) {
+      if (hipEventCreate(&c->epoch) != hipSuccess) return OF_EHIP;
+      c->own_epoch = true;
+    }
+    if (hipEventRecord(c->epoch, c->stream) != hipSuccess) return OF_EHIP;
+  }
   return OF_OK;
 }
 
@@ -1882,6 +1945,20 @@ int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t 
     ++k;
   }
   *n = k;
+  return OF_OK;
+}
+
+int of_kernel_timeline(of_ctx *c, int max, const char **names, double *pixels, double *t0_ms, double *t1_ms,
+                       int *n) {
+  if (!c || !n) return OF_EINVAL;
+  const int m = (int)c->tl.size();
+  for (int k = 0; k < m && k < max; ++k) {
+    if (names) names[k] = c->tl[k].name;
+    if (pixels) pixels[k] = c->tl[k].px;
+    if (t0_ms) t0_ms[k] = c->tl[k].t0;
+    if (t1_ms) t1_ms[k] = c->tl[k].t1;
+  }
+  *n = m;
   return OF_OK;
 }
 
@@ -2072,6 +2149,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
   REQUIRE(P && nslots >= 1 && nslots <= (int)c->slots.size() && lanes >= 1 && lanes <= 16, OF_EINVAL,
           "bad arguments");
   for (int s = 0; s < nslots; ++s) REQUIRE(c->slots[s].rgb1 && c->slots[s].uv, OF_EINVAL, "slot not uploaded");
+  REQUIRE(!c->pool, OF_EINVAL, "a pair stream is open on this context (of_pairs_close first)");
   lanes = std::min(lanes, nslots);
   if (lanes == 1) {
     for (int s = 0; s < nslots; ++s) {
@@ -2085,6 +2163,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
   } else {
     // lane 0 is the ctx itself (its stream), lanes 1.. are child contexts:
     // `lanes` streams in all, within GPU_MAX_HW_QUEUES (4) for lanes <= 4
+    // (of_pairs_run_host adds its copy stream, see HostStage)
     while ((int)c->lanes.size() < lanes - 1) {
       of_ctx *l = nullptr;
       const int rc = of_ctx_create(c->device, &l);
@@ -2102,6 +2181,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
       l->opt_sor_pipe = c->opt_sor_pipe;
+      if (l != c) l->epoch = c->epoch;
       l->big = big_px > 0 ? &c->big_own : nullptr;
       l->big_px = big_px;
       th.emplace_back([c, l, li, lanes, nslots, P, st, &errs] {
@@ -2134,6 +2214,8 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
         d.n += kv.second.n;
       }
       c->lanes[li - 1]->ktimes.clear();
+      c->tl.insert(c->tl.end(), c->lanes[li - 1]->tl.begin(), c->lanes[li - 1]->tl.end());
+      c->lanes[li - 1]->tl.clear();
     }
     for (auto &e : errs)
       if (e.code != OF_OK) throw e;
@@ -2290,6 +2372,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
               lanes >= 1 && lanes <= 16,
           OF_EINVAL, "bad arguments");
   for (int k = 0; k < npairs; ++k) REQUIRE(im1[k] && im2[k] && out_uv[k], OF_EINVAL, "null pair buffer");
+  REQUIRE(!c->pool, OF_EINVAL, "a pair stream is open on this context (of_pairs_close first)");
   if ((int)c->slots.size() < npairs) c->slots.resize(npairs);
   const size_t nu = 2 * (size_t)H * W;
   for (int k = 0; k < npairs; ++k) {
@@ -2330,6 +2413,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
       l->opt_sor_pipe = c->opt_sor_pipe;
+      if (l != c) l->epoch = c->epoch;
       l->big = OF_BIG_PX > 0 ? &c->big_own : nullptr;
       l->big_px = OF_BIG_PX;
       th.emplace_back([=, &errs] {
@@ -2358,11 +2442,280 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
         d.n += kv.second.n;
       }
       c->lanes[li - 1]->ktimes.clear();
+      c->tl.insert(c->tl.end(), c->lanes[li - 1]->tl.begin(), c->lanes[li - 1]->tl.end());
+      c->lanes[li - 1]->tl.clear();
     }
     for (auto &e : errs)
       if (e.code != OF_OK) throw e;
   }
   API_END(c)
+}
+
+// ---- streaming batch: a persistent pool of lanes fed from a queue --------
+namespace {
+struct PairJob {
+  const uint8_t *im1, *im2;
+  float *out;
+  int64_t ticket;
+};
+}  // namespace
+
+struct PairPool {
+  int H = 0, W = 0, C = 0;
+  of_params P;
+  std::vector<of_ctx *> lanes;
+  std::vector<float *> d_uv;  // 2 device flow buffers per lane
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv_job, cv_done;
+  std::deque<PairJob> q;
+  bool closing = false;
+  int64_t next_ticket = 0;
+  std::vector<uint8_t> done;  // by ticket
+  OfError err{OF_OK, ""};
+};
+
+namespace {
+// One lane of the pool: the per-pair pipeline of run_host_lane (pinned and
+// device double buffers, H2D of the next pair and D2H of the previous one on
+// a helper thread while this thread drives a pair's kernels), but pairs come
+// from the pool's queue as they are submitted, so a lane never drains between
+// the caller's chunks.  A pair's flow is written out as soon as no next pair
+// is waiting, so of_pairs_wait never waits for a later submission.
+void pool_lane(of_ctx *c, PairPool *pp, int li) {
+  of_ctx *l = pp->lanes[li];
+  HostStage &h = *l->hs;
+  const int H = pp->H, W = pp->W, C = pp->C;
+  const size_t nb = (size_t)H * W * C, nu = 2 * (size_t)H * W;
+  float *duv[2] = {pp->d_uv[2 * li], pp->d_uv[2 * li + 1]};
+  auto pop = [&](PairJob &j, const bool *stop) {
+    std::unique_lock<std::mutex> lk(pp->m);
+    pp->cv_job.wait(lk, [&] { return !pp->q.empty() || pp->closing || (stop && *stop); });
+    if (pp->q.empty()) return false;
+    j = pp->q.front();
+    pp->q.pop_front();
+    return true;
+  };
+  auto prefetch = [&](int b, const PairJob &j) {
+    HIPCHK(hipEventSynchronize(h.ev_in[b]));
+    memcpy(h.pin_in[b], j.im1, nb);
+    memcpy(h.pin_in[b] + nb, j.im2, nb);
+    HIPCHK(hipEventSynchronize(h.ev_conv[b]));
+    HIPCHK(hipMemcpyAsync(h.d_in[b], h.pin_in[b], 2 * nb, hipMemcpyHostToDevice, h.copy));
+    HIPCHK(hipEventRecord(h.ev_in[b], h.copy));
+  };
+  auto finish = [&](int b, const PairJob &j) {
+    HIPCHK(hipEventSynchronize(h.ev_conv[b]));
+    HIPCHK(hipMemcpyAsync(h.pin_out[b], duv[b], sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
+    HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
+    HIPCHK(hipEventSynchronize(h.ev_out[b]));
+    memcpy(j.out, h.pin_out[b], sizeof(float) * nu);
+    {
+      std::lock_guard<std::mutex> lk(pp->m);
+      pp->done[j.ticket] = 1;
+    }
+    pp->cv_done.notify_all();
+  };
+  PairJob jobs[2];
+  if (!pop(jobs[0], nullptr)) return;
+  prefetch(0, jobs[0]);
+  int b = 0, pending = -1;  // pending: buffer of a computed pair not yet written out
+  for (;;) {
+    l->arena.reset();
+    l->tev_used = 0;
+    HIPCHK(hipStreamWaitEvent(l->stream, h.ev_in[b], 0));
+    Slot s;
+    s.rgb1 = h.d_in[b];
+    s.rgb2 = h.d_in[b] + nb;
+    s.u8 = true;
+    s.uv = duv[b];
+    s.H = H;
+    s.W = W;
+    s.C = C;
+    bool computed = false, got = false;
+    OfError io_err{OF_OK, ""};
+    std::thread io([&, b, pending] {
+      try {
+        HIPCHK(hipSetDevice(l->device));
+        if (pending >= 0) finish(pending, jobs[pending]);
+        got = pop(jobs[b ^ 1], &computed);
+        if (got) prefetch(b ^ 1, jobs[b ^ 1]);
+      } catch (const OfError &e) {
+        io_err = e;
+      }
+    });
+    auto release_io = [&] {
+      {
+        std::lock_guard<std::mutex> lk(pp->m);
+        computed = true;
+      }
+      pp->cv_job.notify_all();
+      io.join();
+    };
+    try {
+      of_params Pc = pp->P;
+      run_slot(l, s, &Pc, nullptr);
+      HIPCHK(hipEventRecord(h.ev_conv[b], l->stream));
+    } catch (...) {
+      release_io();
+      throw;
+    }
+    release_io();
+    if (io_err.code != OF_OK) throw io_err;
+    pending = b;
+    if (!got) {
+      finish(b, jobs[b]);
+      pending = -1;
+      if (!pop(jobs[b ^ 1], nullptr)) return;
+      prefetch(b ^ 1, jobs[b ^ 1]);
+    }
+    b ^= 1;
+  }
+}
+}  // namespace
+
+// Streaming batch (host I/O overlapped with the GPU):
+// of_pairs_open starts `lanes` pipelines (child contexts, one host thread
+// each) that take (H, W, C) uint8 pairs from a queue; of_pairs_submit queues
+// pairs and returns at once; of_pairs_wait blocks until a pair's flow is in
+// the caller's buffer.  Flows equal of_pairs_run_host's with the same lanes
+// (bitwise): lanes == 1 keeps estimate_flow's geometry, lanes >= 2 share the
+// fine-solve token (two pairs' fine CG solves side by side).
+int of_pairs_open(of_ctx *c, int H, int W, int C, const of_params *P, int lanes) {
+  API_BEGIN(c)
+  REQUIRE(!c->pool, OF_EINVAL, "a pair stream is already open on this context");
+  REQUIRE(P && H > 0 && W > 0 && (C == 1 || C == 3) && lanes >= 1 && lanes <= 16, OF_EINVAL, "bad arguments");
+  check_params(P);
+  std::unique_ptr<PairPool> pp(new PairPool());
+  pp->H = H;
+  pp->W = W;
+  pp->C = C;
+  pp->P = *P;
+  const size_t nu = 2 * (size_t)H * W;
+  stage_alloc(c, c, 0, 0);  // the shared copy stream
+  try {
+    for (int li = 0; li < lanes; ++li) {
+      of_ctx *l = nullptr;
+      const int rc = of_ctx_create(c->device, &l);
+      REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
+      pp->lanes.push_back(l);
+      l->prof = 0;
+      l->opt_sor_pipe = c->opt_sor_pipe;
+      l->big = lanes > 1 && OF_BIG_PX > 0 ? &c->big_own : nullptr;
+      l->big_px = OF_BIG_PX;
+      stage_alloc(l, c, 2 * (size_t)H * W * C, nu);
+      for (int b = 0; b < 2; ++b) {
+        float *d = nullptr;
+        HIPCHK(hipMalloc(&d, sizeof(float) * nu));
+        pp->d_uv.push_back(d);
+      }
+    }
+  } catch (...) {
+    for (of_ctx *l : pp->lanes) of_ctx_destroy(l);
+    for (float *d : pp->d_uv) hipFree(d);
+    throw;
+  }
+  PairPool *raw = pp.release();
+  c->pool = raw;
+  for (int li = 0; li < lanes; ++li)
+    raw->th.emplace_back([c, raw, li] {
+      try {
+        HIPCHK(hipSetDevice(raw->lanes[li]->device));
+        pool_lane(c, raw, li);
+      } catch (const OfError &e) {
+        std::lock_guard<std::mutex> lk(raw->m);
+        if (raw->err.code == OF_OK) raw->err = e;
+        raw->closing = true;
+      } catch (const std::exception &e) {
+        std::lock_guard<std::mutex> lk(raw->m);
+        if (raw->err.code == OF_OK) raw->err = OfError{OF_ENOMEM, e.what()};
+        raw->closing = true;
+      }
+      raw->cv_done.notify_all();
+      raw->cv_job.notify_all();
+    });
+  API_END(c)
+}
+
+// queue n pairs (caller-owned (H, W, C) uint8 frames and planar 2 x H x W fp32
+// outputs, all kept alive until waited for); tickets first .. first + n - 1
+int of_pairs_submit(of_ctx *c, int n, const uint8_t *const *im1, const uint8_t *const *im2, float *const *out_uv,
+                    int64_t *first_ticket) {
+  if (!c) return OF_EINVAL;
+  PairPool *pp = c->pool;
+  if (!pp || n < 1 || !im1 || !im2 || !out_uv) {
+    c->err = pp ? "bad arguments" : "no pair stream open (of_pairs_open)";
+    return OF_EINVAL;
+  }
+  for (int k = 0; k < n; ++k)
+    if (!im1[k] || !im2[k] || !out_uv[k]) {
+      c->err = "null pair buffer";
+      return OF_EINVAL;
+    }
+  {
+    std::lock_guard<std::mutex> lk(pp->m);
+    if (pp->err.code != OF_OK) {
+      c->err = pp->err.msg;
+      return pp->err.code;
+    }
+    if (pp->closing) {
+      c->err = "pair stream closing";
+      return OF_EINVAL;
+    }
+    if (first_ticket) *first_ticket = pp->next_ticket;
+    for (int k = 0; k < n; ++k) {
+      pp->q.push_back({im1[k], im2[k], out_uv[k], pp->next_ticket++});
+      pp->done.push_back(0);
+    }
+  }
+  pp->cv_job.notify_all();
+  return OF_OK;
+}
+
+// block until pair `ticket`'s flow has been written (a lane's error is
+// returned here, and by every later call)
+int of_pairs_wait(of_ctx *c, int64_t ticket) {
+  if (!c) return OF_EINVAL;
+  PairPool *pp = c->pool;
+  if (!pp) {
+    c->err = "no pair stream open (of_pairs_open)";
+    return OF_EINVAL;
+  }
+  std::unique_lock<std::mutex> lk(pp->m);
+  if (ticket < 0 || ticket >= pp->next_ticket) {
+    c->err = "unknown ticket";
+    return OF_EINVAL;
+  }
+  pp->cv_done.wait(lk, [&] { return pp->done[ticket] || pp->err.code != OF_OK; });
+  if (!pp->done[ticket]) {
+    c->err = pp->err.msg;
+    return pp->err.code;
+  }
+  return OF_OK;
+}
+
+// finish every queued pair, stop the lanes and release them
+int of_pairs_close(of_ctx *c) {
+  if (!c) return OF_EINVAL;
+  PairPool *pp = c->pool;
+  if (!pp) return OF_OK;
+  {
+    std::lock_guard<std::mutex> lk(pp->m);
+    pp->closing = true;
+  }
+  pp->cv_job.notify_all();
+  for (auto &t : pp->th) t.join();
+  for (of_ctx *l : pp->lanes) of_ctx_destroy(l);
+  hipSetDevice(c->device);
+  for (float *d : pp->d_uv) hipFree(d);
+  const OfError e = pp->err;
+  delete pp;
+  c->pool = nullptr;
+  if (e.code != OF_OK) {
+    c->err = e.msg;
+    return e.code;
+  }
+  return OF_OK;
 }
 
 int of_pair_download(of_ctx *c, int slot, float *out_uv) {
@@ -2593,7 +2946,7 @@ int of_solve_dia(of_ctx *c, const of_params *P, int D, const float *planes, cons
   L.e = new_f2(c, H, W);
   upload_img(c, L.pl, planes);
   F2 b = upload_f2(c, rhs, H, W), xx = new_f2(c, H, W);
-  const SolveResult r = gen_solve(c, P, L, b, xx);
+  const SolveResult r = gen_solve_logged(c, P, L, b, xx);
   download_f2(c, xx, x);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (iters) *iters = r.iters;

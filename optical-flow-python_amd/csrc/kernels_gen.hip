@@ -343,6 +343,7 @@ __global__ __launch_bounds__(1024) void k_dia_sor(DiaArgs a, float omega, int ma
   const int t = threadIdx.x, nt = blockDim.x;
   const int D = a.D, S = 2 * D + 1, G = S * S, e0 = D * S + D, L = D + 1;
   int sweep = 0;
+  bool conv = false;  // the stopping test passed (also on the last allowed sweep)
   for (; sweep < maxit; ++sweep) {
     double dn = 0.0, xn = 0.0;
     for (int comp = 0; comp < 2; ++comp) {
@@ -398,11 +399,12 @@ __global__ __launch_bounds__(1024) void k_dia_sor(DiaArgs a, float omega, int ma
     __syncthreads();
     if (sqrt(sd) < tol * sqrt(sx)) {
       ++sweep;
+      conv = true;
       break;
     }
   }
   if (t == 0) {
     a.st->iter = sweep;
-    a.st->done = sweep < maxit ? 1 : 2;
+    a.st->done = conv ? 1 : 2;
   }
 }

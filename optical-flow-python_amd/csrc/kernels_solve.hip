@@ -1760,6 +1760,30 @@ __device__ __forceinline__ float sor_from_down(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
+// The relaxation of one point (base.py:161-163), x <- (1 - w) x + w (b -
+// sigma) / a_rr with sigma = sum_{c != r} A_rc x_c = -(N x)_r + c x_other,
+// shared by k_sor_lex and k_sor_pipe.  Every multiply-add is an explicit
+// fmaf and the fp64 sums explicit fma: left to the compiler, the two kernels
+// contracted different subsets of the products (the pipelined one packed
+// some into v_pk_mul_f32 + v_add), so their iterates differed in the last
+// bit; spelled out, the rounding is fixed by the source.
+__device__ __forceinline__ float sor_relax(float bb, float wl, float left, float wr, float right, float wd, float down,
+                                           float wu, float up, float cc, float other, float dg, float old, float om,
+                                           float om1) {
+  float sgm = fmaf(wl, left, bb);
+  sgm = fmaf(wr, right, sgm);
+  sgm = fmaf(wd, down, sgm);
+  sgm = fmaf(wu, up, sgm);
+  sgm = fmaf(-cc, other, sgm);
+  return fabsf(dg) < 1e-15f ? old : fmaf(om1, old, (om * sgm) / dg);
+}
+// ||x_new - x_old||^2 and ||x_new||^2 partial sums (fp64)
+__device__ __forceinline__ void sor_acc(float nw, float old, double &dn, double &xn) {
+  const double dd = (double)nw - (double)old;
+  dn = fma(dd, dd, dn);
+  xn = fma((double)nw, (double)nw, xn);
+}
+
 // one strip of one half: PH 0 relaxes u (x.x), PH 1 relaxes v (x.y)
 template <int PH>
 __device__ __forceinline__ void sor_strip(const SorArgs &a, int s, int k, double &dn, double &xn) {
@@ -1835,15 +1859,11 @@ __device__ __forceinline__ void sor_strip(const SorArgs &a, int s, int k, double
         up = PH ? XU[q].y : XU[q].x;
         wu = WYU[q];
       }
-      const float sgm = BB[q] + wx_prev * res + WX[q] * right + WY[q] * down + wu * up - CC[q] * other;
-      const float dg = DG[q];
-      float nw = fabsf(dg) < 1e-15f ? old : om1 * old + om * sgm / dg;
+      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
       if (act) {
         const size_t o = row + j;
         sor_st(a.x + o, PH ? make_float2(other, nw) : make_float2(nw, other));
-        const double dd = (double)nw - (double)old;
-        dn += dd * dd;
-        xn += (double)nw * nw;
+        sor_acc(nw, old, dn, xn);
       } else {
         nw = 0.f;
       }
@@ -2092,15 +2112,11 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
         up = PH ? XU[q].y : XU[q].x;
         wu = WYU[q];
       }
-      const float sgm = BB[q] + wx_prev * res + WX[q] * right + WY[q] * down + wu * up - CC[q] * other;
-      const float dg = DG[q];
-      float nw = fabsf(dg) < 1e-15f ? old : om1 * old + om * sgm / dg;
+      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
       if (act) {
         const size_t o = row + j;
         sor_st(xc + o, PH ? make_float2(other, nw) : make_float2(nw, other));
-        const double dd = (double)nw - (double)old;
-        dn += dd * dd;
-        xn += (double)nw * nw;
+        sor_acc(nw, old, dn, xn);
       } else {
         nw = 0.f;
       }

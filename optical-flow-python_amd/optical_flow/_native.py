@@ -35,6 +35,7 @@ _SIGS = {
     "of_set_profiling": ([_vp, C.c_int], C.c_int),
     "of_set_option": ([_vp, C.c_int, C.c_int], C.c_int),
     "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _dp, _ip], C.c_int),
+    "of_kernel_timeline": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, _dp, _dp, _ip], C.c_int),
     "of_estimate_flow": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, C.c_int, _fp, _fp,
                           C.POINTER(OfStats)], C.c_int),
     "of_compute_flow": ([_vp, C.POINTER(OfParams), _fp, C.c_int, C.c_int, C.c_int, _fp, C.c_int, _fp, _fp,
@@ -49,6 +50,11 @@ _SIGS = {
     "of_pairs_run_host": ([_vp, C.c_int, C.POINTER(_vp), C.POINTER(_vp), C.c_int, C.c_int, C.c_int,
                            C.POINTER(OfParams), C.c_int, C.POINTER(_vp), C.POINTER(OfStats)], C.c_int),
     "of_pair_download": ([_vp, C.c_int, _fp], C.c_int),
+    "of_pairs_open": ([_vp, C.c_int, C.c_int, C.c_int, C.POINTER(OfParams), C.c_int], C.c_int),
+    "of_pairs_submit": ([_vp, C.c_int, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(C.c_int64)],
+                        C.c_int),
+    "of_pairs_wait": ([_vp, C.c_int64], C.c_int),
+    "of_pairs_close": ([_vp], C.c_int),
     "of_rccl_unique_id": ([C.c_char_p], C.c_int),
     "of_rccl_init": ([_vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
     "of_rccl_gather_flows": ([_vp, C.c_int, _fp], C.c_int),

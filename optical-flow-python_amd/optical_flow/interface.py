@@ -58,7 +58,10 @@ def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes
     """estimate_flow over a batch of uint8 frame pairs, host to host: one C
     call (of_pairs_run_host) keeps `lanes` pairs in flight on the GPU with
     their uploads and downloads overlapped.  Returns a list of (H, W, 2)
-    float64 flows equal to [estimate_flow(a, b, method, params) ...]."""
+    float64 flows equal to [estimate_flow(a, b, method, params) ...]:
+    bitwise with lanes=1 or below 2^20 px; at >= 2^20 px with lanes >= 2 the
+    fine CG solves of two pairs run side by side in another block geometry
+    and the flows differ by CG rounding only (include/optflow.h)."""
     a = [_as_u8(x) for x in im1s]
     b = [_as_u8(x) for x in im2s]
     if not a or len(a) != len(b):
@@ -92,6 +95,84 @@ def estimate_flow_batch(im1s, im2s, method='classic+nl-fast', params=None, lanes
     ctx = nat.context()
     ctx.check(ctx.lib.of_pairs_run_host(ctx.handle, n, p1, p2, H, W, Cc, C.byref(P), int(lanes), po, None))
     return [nat.interleaved(o) for o in outs]
+
+
+class PairStream:
+    """Streaming estimate_flow over uint8 frame pairs of one shape: a pool of
+    `lanes` GPU pipelines (of_pairs_open, include/optflow.h) on a context of
+    its own takes pairs as they are submitted, so host work between
+    submissions (decoding, writing) never drains the GPU.  Flows equal
+    estimate_flow_batch(..., lanes=lanes) bitwise.
+
+        with PairStream(H, W, 3, 'classic+nl-fast') as s:
+            t = s.submit(im1, im2)      # returns at once
+            uv = s.wait(t)              # (H, W, 2) float64
+    """
+
+    def __init__(self, H, W, channels=3, method='classic+nl-fast', params=None, lanes=4, device=0):
+        if channels not in (1, 3):
+            raise ValueError("channels must be 1 (gray) or 3 (RGB)")
+        ope = load_of_method(method)
+        if params is not None:
+            ope.parse_input_parameter(params)
+        P = ope.to_params()
+        P.guide_mode = int(ope._METHOD == 'classic_nl' and ope.color_images is not None)
+        self.shape = (H, W, 3) if channels == 3 else (H, W)
+        self.H, self.W, self.channels = H, W, channels
+        self._ctx = nat.Context(device)
+        self._live = {}
+        try:
+            self._ctx.check(self._ctx.lib.of_pairs_open(self._ctx.handle, H, W, channels, C.byref(P), int(lanes)))
+        except Exception:
+            self._ctx.close()
+            raise
+
+    def submit(self, im1, im2):
+        """Queue one pair; returns its ticket.  The frames are copied into the
+        stream's pinned buffers by a lane thread later, so they are kept
+        referenced here until wait()."""
+        a = _as_u8(im1)
+        b = _as_u8(im2)
+        if a.ndim == 3:
+            a, b = np.ascontiguousarray(a[:, :, :3]), np.ascontiguousarray(b[:, :, :3])
+        if a.shape != self.shape or b.shape != self.shape:
+            raise ValueError(f"frames must be {self.shape}, got {a.shape} / {b.shape}")
+        out = np.empty((2, self.H, self.W), dtype=np.float32)
+        vp = C.c_void_p
+        t = C.c_int64(0)
+        self._ctx.check(self._ctx.lib.of_pairs_submit(self._ctx.handle, 1, (vp * 1)(a.ctypes.data),
+                                                      (vp * 1)(b.ctypes.data), (vp * 1)(out.ctypes.data),
+                                                      C.byref(t)))
+        self._live[t.value] = (a, b, out)
+        return t.value
+
+    def wait(self, ticket):
+        """Block until the pair's flow is ready; (H, W, 2) float64."""
+        if ticket not in self._live:
+            raise ValueError(f"unknown or already waited ticket {ticket}")
+        self._ctx.check(self._ctx.lib.of_pairs_wait(self._ctx.handle, int(ticket)))
+        return nat.interleaved(self._live.pop(ticket)[2])
+
+    def close(self):
+        if self._ctx is not None:
+            try:
+                self._ctx.check(self._ctx.lib.of_pairs_close(self._ctx.handle))
+            finally:
+                self._ctx.close()
+                self._ctx = None
+                self._live.clear()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _preprocess(im1, im2):

@@ -15,8 +15,9 @@ overlapped with the GPU:
 
 Pairs are grouped by frame shape (Middlebury sequences differ in size) and
 results come back in job order.  Each flow equals `estimate_flow(im1, im2,
-method, params)` on the decoded frames (the batch entry is bitwise equal to
-per-pair calls and independent of `lanes`).
+method, params)` on the decoded frames: bitwise below 2^20 px, and to CG
+rounding at >= 2^20 px with lanes >= 2, where two pairs' fine solves run side
+by side in another block geometry (include/optflow.h, of_pairs_run).
 """
 import os
 import threading
@@ -88,7 +89,7 @@ def _finish(job, uv, gt, border):
 
 
 def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, workers=4, writers=2, border=0,
-                 keep_flows=False, flow_fn=None):
+                 keep_flows=False, flow_fn=None, stream=True):
     """Run `jobs` (PairJob list) through decode -> flow -> write + metrics
     with the three stages overlapped.  Returns (results, stats): one dict
     per job in job order ({name, shape, out, [aae, std_ae, aepe], [uv]}) and
@@ -96,11 +97,17 @@ def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, 
     (decode_s / write_s are busy times summed over their `workers` /
     `writers` threads, so overlap shows as gpu_s ~ wall_s).  `flow_fn(im1s, im2s)` replaces the GPU batch
     call (host-logic tests); by default estimate_flow_batch(..., method,
-    params, lanes)."""
+    params, lanes) per chunk, or with `stream` (the default when no flow_fn
+    is given) every decoded pair goes straight into a PairStream of its
+    shape (of_pairs_submit), at most 2 lanes + 2 pairs per stream in flight,
+    so the GPU lanes never drain between chunks; gpu_s is then the time this
+    thread waited for flows."""
     if not jobs:
         return [], {"pairs": 0, "wall_s": 0.0, "pairs_per_s": 0.0, "decode_s": 0.0, "gpu_s": 0.0, "write_s": 0.0}
     if chunk < 1 or workers < 1 or writers < 1:
         raise ValueError("chunk, workers and writers must be >= 1")
+    if flow_fn is None and stream:
+        return _run_streaming(jobs, method, params, lanes, chunk, workers, writers, border, keep_flows)
     if flow_fn is None:
         from optical_flow.interface import estimate_flow_batch
 
@@ -159,5 +166,81 @@ def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, 
                 results[i]["uv"] = uv
     wall = time.perf_counter() - t_start
     stats = {"pairs": len(jobs), "wall_s": wall, "pairs_per_s": len(jobs) / wall if wall > 0 else 0.0}
+    stats.update(busy)
+    return results, stats
+
+
+def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, border, keep_flows, max_streams=2):
+    """run_pipeline's streaming form: decode pool -> PairStream per frame
+    shape (at most `max_streams` open; the least recently used one is drained
+    and closed) -> writer pool, results in job order."""
+    from optical_flow.interface import PairStream
+    t_start = time.perf_counter()
+    lock = threading.Lock()
+    busy = {"decode_s": 0.0, "write_s": 0.0, "gpu_s": 0.0}
+
+    def timed(key, fn, *a):
+        t0 = time.perf_counter()
+        try:
+            return fn(*a)
+        finally:
+            with lock:
+                busy[key] += time.perf_counter() - t0
+
+    streams = {}    # shape -> PairStream, in least-recently-used order
+    inflight = {}   # shape -> [(job index, ticket, ground truth)]
+    window = 2 * lanes + 2
+    results = [None] * len(jobs)
+    writes = []
+    with ThreadPoolExecutor(workers) as dec, ThreadPoolExecutor(writers) as wr:
+        futs = [None] * len(jobs)
+        nsub = 0
+        ahead = 2 * max(1, ahead_chunks)
+
+        def submit_upto(n):
+            nonlocal nsub
+            while nsub < min(n, len(jobs)):
+                futs[nsub] = dec.submit(timed, "decode_s", decode_pair, jobs[nsub])
+                nsub += 1
+
+        def retire(shape):
+            i, t, gt = inflight[shape].pop(0)
+            uv = timed("gpu_s", streams[shape].wait, t)
+            writes.append((i, wr.submit(timed, "write_s", _finish, jobs[i], uv, gt, border), uv if keep_flows else None))
+
+        def close(shape):
+            while inflight[shape]:
+                retire(shape)
+            streams.pop(shape).close()
+            del inflight[shape]
+
+        try:
+            for i in range(len(jobs)):
+                submit_upto(i + ahead)
+                a, b, gt = futs[i].result()
+                futs[i] = None
+                shape = a.shape
+                if shape not in streams:
+                    if len(streams) >= max_streams:
+                        close(next(iter(streams)))
+                    streams[shape] = PairStream(shape[0], shape[1], 3 if a.ndim == 3 else 1, method, params, lanes)
+                    inflight[shape] = []
+                else:
+                    streams[shape] = streams.pop(shape)  # most recently used last
+                inflight[shape].append((i, streams[shape].submit(a, b), gt))
+                while len(inflight[shape]) > window:
+                    retire(shape)
+            for shape in list(streams):
+                close(shape)
+        finally:
+            for st in streams.values():
+                st.close()
+        for i, f, uv in writes:
+            results[i] = f.result()
+            if keep_flows:
+                results[i]["uv"] = uv
+    wall = time.perf_counter() - t_start
+    stats = {"pairs": len(jobs), "wall_s": wall, "pairs_per_s": len(jobs) / wall if wall > 0 else 0.0,
+             "stream": True}
     stats.update(busy)
     return results, stats

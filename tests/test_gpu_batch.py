@@ -155,6 +155,10 @@ def test_pairs_run_host_fine_solves_side_by_side():
     for k in range(3):
         assert np.array_equal(got2[k], got3[k]), k
     ref = optical_flow.estimate_flow(pairs[0][0], pairs[0][1], "classic+nl-fast")
+    # the documented contract (include/optflow.h, of_pairs_run_host): one
+    # lane keeps estimate_flow's single-solve geometry, bitwise
+    got1 = optical_flow.estimate_flow_batch(a[:1], b[:1], "classic+nl-fast", lanes=1)
+    assert np.array_equal(got1[0], ref)
     e = np.sqrt(((got2[0] - ref) ** 2).sum(-1))
     aepe = lambda uv: float(np.sqrt(((uv - pairs[0][2]) ** 2).sum(-1)).mean())  # noqa: E731
     print(f"lanes vs single 1080p: mean {e.mean():.2e} p99 {np.percentile(e, 99):.2e} "

@@ -111,3 +111,28 @@ def test_e2e_general_filters(golden, tag, tol):
     print(tag, s)
     assert np.all(np.isfinite(uv))
     assert s["mean"] <= tol[0] and s["median"] <= tol[1], s
+
+
+def test_general_filter_solves_logged(golden):
+    """Solves of a general spatial_filters list go through the DIA path
+    (gen_solve) and are recorded by the solve log like the 5-point ones, with
+    their fp64 true residual: 'backslash' meets its 1e-6 goal (iterative
+    refinement on that residual)."""
+    import optical_flow
+    from optical_flow import _native
+    d = golden("filters.npz")
+    o = _method("diag4")
+    prm = {"spatial_filters": o.spatial_filters, "rho_spatial_u": o.rho_spatial_u, "rho_spatial_v": o.rho_spatial_v}
+    ctx = _native.context()
+    ctx.set_solve_log(True)
+    try:
+        optical_flow.estimate_flow(d["im1"], d["im2"], METH["diag4"], prm)
+        recs = ctx.solve_log()
+    finally:
+        ctx.set_solve_log(False)
+    assert len(recs) > 0
+    for r in recs:
+        print(r)
+    assert all(r["solver"] == 0 and r["done"] in (1, 3) for r in recs)
+    assert max(r["true_rel"] for r in recs) <= 1.5e-6
+    assert all(r["true_rel_out"] == r["true_rel"] for r in recs)

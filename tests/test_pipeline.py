@@ -94,7 +94,8 @@ def test_middlebury_jobs_layout(tmp_path):
 
 
 @pytest.mark.gpu
-def test_pipeline_gpu_matches_estimate_flow(tmp_path):
+@pytest.mark.parametrize("stream", [True, False])
+def test_pipeline_gpu_matches_estimate_flow(tmp_path, stream):
     """Real path: RubberWhale (Middlebury layout built from the committed
     frames + GT) and synthetic pairs of two other sizes, RGB and gray, chunk
     2, 3 lanes.  Every written .flo equals estimate_flow on the decoded
@@ -114,7 +115,9 @@ def test_pipeline_gpu_matches_estimate_flow(tmp_path):
     syn = tmp_path / "syn"
     syn.mkdir()
     jobs += _write_pairs(syn, [(40, 56, 3), (48, 64, 1), (40, 56, 3), (40, 56, 3)], seed=5)
-    res, st = run_pipeline(jobs, lanes=3, chunk=2, keep_flows=True)
+    # three frame shapes: the streaming form keeps at most two PairStreams
+    # open and closes the least recently used one
+    res, st = run_pipeline(jobs, lanes=3, chunk=2, keep_flows=True, stream=stream)
     print(f"pipeline: {st}")
     for j, r in zip(jobs, res):
         im1 = np.array(Image.open(j.im1)).astype(np.float64)
@@ -127,3 +130,35 @@ def test_pipeline_gpu_matches_estimate_flow(tmp_path):
     rw = res[0]
     print(f"RubberWhale AAE {rw['aae']:.5f} AEPE {rw['aepe']:.6f} (reference 2.46298 / 0.080250)")
     assert abs(rw["aepe"] - 0.080250) <= 1e-3 and abs(rw["aae"] - 2.46298) <= 0.02
+
+
+@pytest.mark.gpu
+def test_pair_stream_matches_batch():
+    """PairStream (of_pairs_open / submit / wait / close): pairs submitted one
+    by one and waited out of order give bitwise the flows of
+    estimate_flow_batch with the same lanes; bad frames and tickets raise."""
+    import optical_flow
+    from optical_flow.utils.synthetic import synth_pair
+    pairs = [synth_pair(60, 88, 30 + k) for k in range(5)]
+    a = [p[0].astype(np.uint8) for p in pairs]
+    b = [p[1].astype(np.uint8) for p in pairs]
+    want = optical_flow.estimate_flow_batch(a, b, "classic+nl-fast", lanes=2)
+    with optical_flow.PairStream(60, 88, 3, "classic+nl-fast", lanes=2) as s:
+        t = [s.submit(x, y) for x, y in zip(a, b)]
+        got = {k: s.wait(t[k]) for k in (3, 0, 4, 1, 2)}
+        with pytest.raises(ValueError):
+            s.submit(a[0][:, :-1], b[0][:, :-1])
+        with pytest.raises(ValueError):
+            s.wait(t[0])  # already waited
+        t5 = s.submit(a[2], b[2])
+        late = s.wait(t5)
+    for k in range(5):
+        np.testing.assert_array_equal(got[k], want[k])
+    np.testing.assert_array_equal(late, want[2])
+    # gray frames, one lane: bitwise estimate_flow
+    g1 = [np.round(x.mean(-1)).astype(np.uint8) for x in a[:2]]
+    g2 = [np.round(x.mean(-1)).astype(np.uint8) for x in b[:2]]
+    with optical_flow.PairStream(60, 88, 1, "hs", lanes=1) as s:
+        uv = [s.wait(s.submit(x, y)) for x, y in zip(g1, g2)]
+    for k in range(2):
+        np.testing.assert_array_equal(uv[k], optical_flow.estimate_flow(g1[k].astype(float), g2[k].astype(float), "hs"))

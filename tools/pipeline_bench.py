@@ -56,13 +56,19 @@ def main():
     mem = a.pairs / (time.perf_counter() - t0)
     res, st = run_pipeline(jobs, lanes=a.lanes, chunk=a.chunk, workers=a.workers, writers=a.writers)
     aepe = float(np.mean([r["aepe"] for r in res]))
+    # the round-3 form: chunks of `chunk` pairs per of_pairs_run_host call
+    res_c, st_c = run_pipeline(jobs, lanes=a.lanes, chunk=a.chunk, workers=a.workers, writers=a.writers,
+                               stream=False)
+    assert all(np.array_equal(r.get("aepe"), q.get("aepe")) for r, q in zip(res, res_c))
     print(json.dumps({"metric": "file-to-file pairs/s (PNG decode -> flow -> .flo + AAE/AEPE)",
                       "value": round(st["pairs_per_s"], 3), "in_memory_pairs_per_s": round(mem, 3),
                       "pairs": a.pairs, "height": a.height, "width": a.width, "lanes": a.lanes, "chunk": a.chunk,
                       "workers": a.workers, "writers": a.writers,
                       "wall_s": round(st["wall_s"], 3), "gpu_busy_s": round(st["gpu_s"], 3),
                       "decode_busy_s": round(st["decode_s"], 3), "write_busy_s": round(st["write_s"], 3),
-                      "mean_aepe_gt": round(aepe, 5)}), flush=True)
+                      "mean_aepe_gt": round(aepe, 5), "mode": "stream (of_pairs_submit / of_pairs_wait)",
+                      "chunked": {"value": round(st_c["pairs_per_s"], 3), "wall_s": round(st_c["wall_s"], 3),
+                                  "gpu_busy_s": round(st_c["gpu_s"], 3)}}), flush=True)
     if not a.out:
         shutil.rmtree(tmp, ignore_errors=True)
 

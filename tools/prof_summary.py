@@ -4,6 +4,9 @@ and the algorithmic-bytes roofline.  Writes <dir>/summary.json and, with
 --traffic, profiles/pmc_traffic.json (read by bench.py).
 
 usage: python tools/prof_summary.py gpurun_out/prof_TAG [--H 1080 --W 1920] [--traffic]
+       [--workload classic+nl-fast@1080x1920/backslash]
+The traffic file is keyed by workload (bench.py's method@HxW/solver), then
+by bench kernel name, each record naming the kernel symbol it measured.
 """
 import argparse
 import collections
@@ -53,6 +56,8 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--traffic", action="store_true")
+    ap.add_argument("--workload", default="classic+nl-fast@1080x1920/backslash")
+    ap.add_argument("--source", default=None, help="note stored with the records (e.g. the profile tag)")
     a = ap.parse_args()
     import bench  # noqa: E402  (KERNEL_BYTES_PER_PX, profiler names)
     d = a.dir
@@ -113,8 +118,9 @@ def main():
         hk, mk = Hh.get((n, g), []), M.get((n, g), [])
         if hk and mk and sum(hk) + sum(mk) > 0:
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
-        key = {"k_cgs": "pcg_iter", "k_cgp": "pcg_iter", "k_flow_operator": "flow_operator", "k_wmf": "wmf", "k_rof_iters": "rof_iters",
-               "k_update_occ": "update_occ", "k_partial_deriv<1>": "partial_deriv_hermite"}.get(n)
+        key = {"k_cgs": "pcg_iter", "k_cgp": "pcg_iter", "k_cg": "pcg_iter", "k_flow_operator": "flow_operator",
+               "k_wmf": "wmf", "k_rof_iters": "rof_iters", "k_update_occ": "update_occ",
+               "k_partial_deriv<1>": "partial_deriv_hermite", "k_sor_pipe": "sor_pipe", "k_sor_lex": "sor_sweep"}.get(n)
         if key in bench.KERNEL_BYTES_PER_PX:
             px = a.H * a.W * (2 if key == "rof_iters" else 1)
             alg = bench.KERNEL_BYTES_PER_PX[key] * px
@@ -138,17 +144,20 @@ def main():
     for n, r in list(out.items())[:14]:
         print(f"{n[:34]:34s} {json.dumps(r)}")
     if a.traffic:
-        traffic = {r["bench_name"]: {"hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"),
-                                     "hbm_bytes_per_launch_all": r.get("hbm_bytes_per_launch_all"),
-                                     "fetch_MB": r.get("fetch_MB"),
-                                     "write_MB": r.get("write_MB"), "grid": r["finest_grid"],
-                                     "l2_hit": r.get("l2_hit"),
-                                     "valu_insts_per_launch": r.get("valu_insts_per_launch"),
-                                     "note": "2*FETCH_SIZE + WRITE_SIZE (KB->B) per dispatch at the finest level "
-                                             "(FETCH_SIZE x2: gfx950 tallies 128-B requests at 64 B); "
-                                             "Infinity-Cache (MALL) hits are included in FETCH_SIZE"}
-                   for r in out.values() if "bench_name" in r}
+        recs = {r["bench_name"]: {"symbol": n, "source": a.source or os.path.basename(os.path.normpath(d)),
+                                  "hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"),
+                                  "hbm_bytes_per_launch_all": r.get("hbm_bytes_per_launch_all"),
+                                  "fetch_MB": r.get("fetch_MB"),
+                                  "write_MB": r.get("write_MB"), "grid": r["finest_grid"],
+                                  "l2_hit": r.get("l2_hit"),
+                                  "valu_insts_per_launch": r.get("valu_insts_per_launch"),
+                                  "note": "2*FETCH_SIZE + WRITE_SIZE (KB->B) per dispatch at the finest level "
+                                          "(FETCH_SIZE x2: gfx950 tallies 128-B requests at 64 B); "
+                                          "Infinity-Cache (MALL) hits are included in FETCH_SIZE"}
+                for n, r in out.items() if "bench_name" in r}
         p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+        traffic = json.load(open(p)) if os.path.exists(p) else {}
+        traffic[a.workload] = recs
         json.dump(traffic, open(p, "w"), indent=1)
 
 
