@@ -164,7 +164,13 @@ struct HostStage {
 // k_sor_pipe: persistent grid of one wave per CU; sync words (ticket, fail,
 // stop, counters, decisions, progress stamps) then per-strip partials and the
 // decided sweeps' sums
+#ifndef OF_SOR_PIPE_WAVES
 #define OF_SOR_PIPE_WAVES 256
+#endif
+// dynamic LDS of a k_sor_pipe wave (unused): bounds the waves per CU
+#ifndef OF_SOR_PIPE_SHM
+#define OF_SOR_PIPE_SHM OF_SOR_SHM
+#endif
 #define OF_SORP_SYNC_BYTES (1024 + SOR_RING_MAX * 2 * SOR_MAXS * sizeof(int))
 #define OF_SORP_BYTES (OF_SORP_SYNC_BYTES + (SOR_RING_MAX * 2 * SOR_MAXS * 2 + SOR_RING_MAX * 2) * sizeof(double))
 
@@ -1021,8 +1027,10 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     q.maxiter = P->sor_max_iters;
     HIPCHK(hipMemsetAsync(z, 0, OF_SORP_SYNC_BYTES, c->stream));
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)q.stop, 0x7fffffff, 1, c->stream));
-    const int nwaves = (int)std::min<int64_t>(OF_SOR_PIPE_WAVES, (int64_t)a.maxiter * 2 * nstrips);
-    launch(c, "sor_pipe", k_sor_pipe, dim3(nwaves), dim3(64), OF_SOR_SHM, q);
+    // enough waves for S sweeps in flight (more would only poll)
+    const int nwaves =
+        (int)std::min<int64_t>(std::min(OF_SOR_PIPE_WAVES, 2 * nstrips * S), (int64_t)a.maxiter * 2 * nstrips);
+    launch(c, "sor_pipe", k_sor_pipe, dim3(nwaves), dim3(64), OF_SOR_PIPE_SHM, q);
     Grid2 g = grid2(H, W);
     launch(c, "sor_final", k_sor_pipe_final, g.grid, g.block, 0, q, x.p, c->d_state);
     HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
@@ -1835,7 +1843,7 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipMalloc(&c->d_rpart, sizeof(double) * 2 * PCG_MAX_BLOCKS));
     HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 4 * OF_SLOG_MAX));
     HIPCHK(hipFuncSetAttribute((const void *)k_sor_lex, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
-    HIPCHK(hipFuncSetAttribute((const void *)k_sor_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
+    HIPCHK(hipFuncSetAttribute((const void *)k_sor_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_PIPE_SHM));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
     HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));

@@ -392,6 +392,48 @@ def gen_altba():
     save("altba.npz", **out)
 
 
+def gen_altba_sys():
+    """The first warp's linear system of AltBA compute_flow_base on the
+    altba.npz level (alt_ba.py:214-243), alpha = 0 and 1: the inputs (uv,
+    uvhat, It, Ix, Iy from the reference's partial_deriv, lambda2 = 1e-4),
+    the reference's flow_operator A (COO) and b before the coupling term, the
+    coupling diagonal, and spsolve of the full system (fp64) and of it
+    rounded to float32 (the float32 floor).  Separates solver error from
+    assembly error of the GPU's AltBA path (tools/altba_gpu_probe.py)."""
+    import copy
+    from scipy import sparse
+    from optical_flow.utils.derivatives import partial_deriv
+    d = np.load(os.path.join(HERE, "altba.npz"))
+    out = {}
+    for alpha in (0.0, 1.0):
+        o = ref_cfg.load_of_method("classic-c-a")
+        o.images = d["base_images"]
+        o.lambda2 = 0.01
+        o.max_iters = 4
+        o.alpha = alpha
+        uv, uvhat = d["base_uv"].copy(), d["base_uvhat"].copy()
+        It, Ix, Iy = partial_deriv(o.images, uv, o.interpolation_method, o.deriv_filter)
+        qua = copy.copy(o)
+        qua.lambda_ = o.lambda_q
+        qua.rho_spatial_u = [RobustFunction('quadratic', 1) for _ in o.rho_spatial_u]
+        qua.rho_spatial_v = [RobustFunction('quadratic', 1) for _ in o.rho_spatial_v]
+        qua.rho_data = RobustFunction('quadratic', 1)
+        A, b, _, _ = (qua if alpha == 1 else o).flow_operator(uv, np.zeros_like(uv), It, Ix, Iy)
+        lam2 = 1e-4
+        tmp = o.rho_couple.deriv_over_x(uv.ravel(order='F') - uvhat.ravel(order='F'))
+        Af = (A + lam2 * sparse.diags(tmp, 0, shape=A.shape)).tocsc()
+        bf = b + lam2 * tmp * (uvhat.ravel(order='F') - uv.ravel(order='F'))
+        t = f"a{int(alpha)}_"
+        A = sparse.coo_matrix(A)
+        out[t + "row"], out[t + "col"], out[t + "val"], out[t + "b"] = A.row.astype(np.int32), A.col.astype(np.int32), A.data, b
+        out[t + "couple"], out[t + "bfull"] = lam2 * tmp, bf
+        out[t + "x64"] = spsolve(Af, bf)
+        out[t + "x32"] = spsolve(Af.astype(np.float32).astype(np.float64).tocsc(), bf.astype(np.float32).astype(np.float64))
+        out[t + "It"], out[t + "Ix"], out[t + "Iy"] = It, Ix, Iy
+    out["uv"], out["uvhat"] = d["base_uv"], d["base_uvhat"]
+    save("altba_sys.npz", **out)
+
+
 def gen_viz_metrics():
     """flow_to_color (viz/flow_color.py:43-107) and flow_angular_error
     (metrics.py:5-53) on RubberWhale's ground truth (7244 unknown-flow

@@ -13,4 +13,5 @@ tools/gpu_step.sh 300 gpurun_out/${TAG}_new_tests.log $T tests/test_reference_ho
     tests/test_gpu_filters.py tests/test_gpu_e2e.py -m gpu -k "not rubberwhale" && \
 tools/gpu_step.sh 200 gpurun_out/${TAG}_smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" && \
 tools/gpu_step.sh 400 gpurun_out/${TAG}_cfg2_test.log $T tests/test_gpu_fullsize.py -k "cfg2" && \
-tools/gpu_step.sh 300 gpurun_out/${TAG}_bench_cfg2.log python -u bench.py --method hs --solver sor --height 480 --width 640
+tools/gpu_step.sh 300 gpurun_out/${TAG}_bench_cfg2.log python -u bench.py --method hs --solver sor --height 480 --width 640 && \
+tools/gpu_step.sh 200 gpurun_out/${TAG}_altba_probe.log python -u tools/altba_gpu_probe.py
