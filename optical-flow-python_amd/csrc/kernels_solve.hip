@@ -236,7 +236,9 @@ __device__ __forceinline__ CgInv cg_inv(const CgCoef &c) {
     float id = fabsf(d) > 1e-12f ? __builtin_amdgcn_rcpf(d) : 0.f;
     float ic = 0.f;
     if (BLOCK) {
-      const float det = a * d - cc * cc;
+      // explicit fma: the same rounding wherever the inverse is formed
+      // (k_cgs forms it in two places, CGS_REC_SPLIT)
+      const float det = __builtin_fmaf(a, d, -(cc * cc));
       const bool ok = det > 1e-30f * fabsf(a * d);
       const float inv = __builtin_amdgcn_rcpf(det);
       ia = ok ? d * inv : ia;
@@ -1154,13 +1156,27 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 // from one barrier per step: a stage reads rows of another wave produced at
 // earlier steps; the band is walked for n in [r0 - 8, r1 + 11] so that every
 // row a required stage reads was produced.
-#define CGS_NREC 14
+// CGS_REC_SPLIT (default): wave 0 stores each coefficient row's record RAW
+// (edge weights final, the 2x2 block D as loaded) one row ahead, and wave 3
+// turns it into D^-1 in place one step later, so the inverse (a reciprocal
+// and ~12 multiplies per pixel pair) leaves wave 0, which set the pace of
+// the row step (round-3 phase timing: wave 0 102 K working cycles per
+// launch, wave 3 56 K).  The ring then holds one more row, and wave 0's
+// coefficient loads run one row further ahead (CGS_PF 3) so that a row's
+// load is still two steps from its first use.  Off (0): round 3's layout.
+#ifndef CGS_REC_SPLIT
+#define CGS_REC_SPLIT (!CGS_PAIR)
+#endif
+#if CGS_REC_SPLIT && CGS_PAIR
+#error "CGS_REC_SPLIT does not form the CGS_PAIR Schur complement"
+#endif
+#define CGS_NREC (CGS_REC_SPLIT ? 15 : 14)
 // Load distance in row steps (each step ends at a block barrier, so a load
 // issued at step n is waited for at step n + distance): wave 0's coefficient,
 // p_old and r_in rows (CGS_PF), wave 2's p_old and x rows (CGS_PF2).  Ring
 // sizes are powers of two dividing the 8-step unroll.
 #ifndef CGS_PF
-#define CGS_PF 2
+#define CGS_PF (CGS_REC_SPLIT ? 3 : 2)
 #endif
 #ifndef CGS_PF2
 #define CGS_PF2 1
@@ -1290,6 +1306,26 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
     q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
   };
+  // CGS_REC_SPLIT: the record with D still raw (a, c, c, d) in its D^-1 slots
+  auto put_raw = [&](int t, const CgRaw &c) {
+    float4 *q = &ring[rslot(t)][0][lane];
+    q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
+    q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
+    q[128] = make_float4(c.a.x, c.c.x, c.c.x, c.d.x);
+    q[192] = make_float4(c.a.y, c.c.y, c.c.y, c.d.y);
+  };
+  // ... and its conversion to D^-1 (the same cg_inv as put_rec)
+  auto convert_rec = [&](int t) {
+    float4 *q = &ring[rslot(t)][0][lane];
+    const float4 r0 = q[128], r1 = q[192];
+    CgCoef cc;
+    cc.a = cg_f2{r0.x, r1.x};
+    cc.c = cg_f2{r0.y, r1.y};
+    cc.d = cg_f2{r0.w, r1.w};
+    const CgInv mi = cg_inv<true>(cc);
+    q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
+    q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
+  };
   auto get_rec = [&](int t) {
     const float4 *q = &ring[rslot(t)][0][lane];
     const float4 a = q[0], b = q[64], c = q[128], d = q[192];
@@ -1375,6 +1411,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     if (role == 0) {
       put_rec(ns - 2, SGp[0]);
       put_rec(ns - 1, SGp[1]);
+      if (CGS_REC_SPLIT) put_raw(ns, SG[0]);  // wave 3 converts it at step ns
     }
     __syncthreads();
     CGS_T0
@@ -1410,7 +1447,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         load_raw(n + CGS_PF, SG[RSG(CGS_PF)]);
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
         RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
-        put_rec(n, SG[RSG(0)]);
+        if (CGS_REC_SPLIT) put_raw(n + 1, SG[RSG(1)]);
+        else put_rec(n, SG[RSG(0)]);
         // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
         const CgRec q1 = get_rec(n - 1);
         cg_f2 wu[2];
@@ -1518,6 +1556,9 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       // lower pixel)
       cg_f4 V1[4] = {zero4, zero4, zero4, zero4}, V2[2] = {zero4, zero4};
       CGS_STEPS({
+        // row n's record: raw since wave 0 stored it at step n - 1; stage A
+        // reads it at step n + 1
+        if (CGS_REC_SPLIT) convert_rec(n);
         {
           const CgRec q6 = get_rec(n - 11);
           cg_f2 wu[2];
