@@ -562,7 +562,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // LDS: chunk sums [2][WMF_NC][64] f64 (u chunks, then v chunks; a chunk's
   // 64 lane slots are contiguous, so a scatter-add never conflicts) | records
   // [RW][RP] | sorted positions (ry << 8 | rx) of the u and v lists [2][N] u16 |
-  // chunk ids [2][RW][RP] u8 (u list, v list)
+  // chunk ids [RW][RP][2] u8 (u list, v list of a sample side by side: the
+  // window pass reads both with one u16 load)
   extern __shared__ double lds_f64[];
   wmf_sum_t *csum = reinterpret_cast<wmf_sum_t *>(lds_f64);
   T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
@@ -601,8 +602,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const unsigned pa = (uint16_t)a[r], pb = (uint16_t)b[r];
     ku[e] = (uint16_t)pa;  // padding keys -> 0xffff: out of every window
     kv[e] = (uint16_t)pb;
-    if (pa != 0xffffu) cid[(pa >> 8) * RP + (pa & 0xffu)] = (uint8_t)(e / CH);
-    if (pb != 0xffffu) cid[RW * RP + (pb >> 8) * RP + (pb & 0xffu)] = (uint8_t)(e / CH);
+    if (pa != 0xffffu) cid[2 * ((pa >> 8) * RP + (pa & 0xffu))] = (uint8_t)(e / CH);
+    if (pb != 0xffffu) cid[2 * ((pb >> 8) * RP + (pb & 0xffu)) + 1] = (uint8_t)(e / CH);
   }
   __syncthreads();
   WMF_STAMP(2);
@@ -629,8 +630,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     for (int dx = 0; dx < MX; ++dx)
       if (dx < n) {
         rec[dx] = smp[q0 + dx];
-        cu[dx] = cid[q0 + dx];
-        cv[dx] = cid[RW * RP + q0 + dx];
+        const unsigned pr = reinterpret_cast<const uint16_t *>(cid)[q0 + dx];
+        cu[dx] = pr & 0xffu;
+        cv[dx] = pr >> 8;
       }
 #pragma unroll
     for (int dx = 0; dx < MX; ++dx)

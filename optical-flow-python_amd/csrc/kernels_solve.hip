@@ -1171,6 +1171,14 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #error "CGS_REC_SPLIT does not form the CGS_PAIR Schur complement"
 #endif
 #define CGS_NREC (CGS_REC_SPLIT ? 15 : 14)
+// CGS_E_RAWD: wave 2 loads the raw 2x2 block D (a, c, d planes) of stage E's
+// row itself (L2-resident: wave 0 read it 9 steps earlier) instead of
+// re-forming D from the record's D^-1 (two reciprocals, ~20 VALU per pixel
+// pair).  q = A p is then formed from the exact operator; the iterate differs
+// from the re-formed-D one in the last bits.
+#ifndef CGS_E_RAWD
+#define CGS_E_RAWD 0
+#endif
 // Load distance in row steps (each step ends at a block barrier, so a load
 // issued at step n is waited for at step n + distance): wave 0's coefficient,
 // p_old and r_in rows (CGS_PF), wave 2's p_old and x rows (CGS_PF2).  Ring
@@ -1382,6 +1390,13 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   // rings indexed by (row - ns) mod ring size)
   CgRaw SG[CGS_SGN], SGp[2];
   cg_f4 PO[8], RI[CGS_RIN], PO2[CGS_W2N], XI[CGS_W2N];
+  CgRaw RD[CGS_E_RAWD ? CGS_W2N : 1];  // wave 2: raw a, c, d of stage E's rows
+  auto load_acd = [&](int t, CgRaw &c) {
+    const unsigned v = o4(t);
+    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
+    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
+    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
+  };
   if (live && role == 0) {
     load_raw(ns - 2, SGp[0]);
     load_raw(ns - 1, SGp[1]);
@@ -1398,6 +1413,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     for (int m = -8; m < CGS_PF2 - 8; ++m) {
       PO2[(m + 16) & (CGS_W2N - 1)] = load_po(ns + m);
       XI[(m + 16) & (CGS_W2N - 1)] = load_x(ns + m);
+      if (CGS_E_RAWD) load_acd(ns + m - 1, RD[(m - 1 + 16) & (CGS_W2N - 1)]);
     }
   }
   float alpha = 0.f, beta = 0.f;
@@ -1509,6 +1525,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       CGS_STEPS({
         PO2[RW2(CGS_PF2 - 8)] = load_po(n + CGS_PF2 - 8);
         XI[RW2(CGS_PF2 - 8)] = load_x(n + CGS_PF2 - 8);
+        if (CGS_E_RAWD) load_acd(n + CGS_PF2 - 9, RD[RW2(CGS_PF2 - 9)]);
         // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
           const CgRec q4 = get_rec(n - 8);
@@ -1538,7 +1555,8 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 10, wu);
           const cg_f4 pm = PP[R4(-9)];
-          const cg_f4 q = cgr_diag_p(q5, pm) - cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
+          const cg_f4 q = (CGS_E_RAWD ? cgr_diag_raw(RD[RW2(-9)], pm) : cgr_diag_p(q5, pm)) -
+                          cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
           const cg_f4 yq = cgr_pinv(q5, q);
           st4(s_yq, n - 9, yq);
           const int o = n - 9;
