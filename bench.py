@@ -78,6 +78,7 @@ def parse():
     ap.add_argument("--solver", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-stream", action="store_true", help="skip the streamed (pair pool) rate")
     ap.add_argument("--cpu-sample", type=int, default=360, help="crop height of the CPU-baseline sample")
     return ap.parse_args()
 
@@ -464,6 +465,45 @@ def main():
     value = world * args.pairs * args.steps / elapsed
     gather = gather_check(dist, ctx, lib, world, rank, args.pairs, H, W, outs) if world > 1 else None
 
+    # streamed rate: the same steps through the persistent pair pool
+    # (of_pairs_open / submit / wait, include/optflow.h), step s+1 submitted
+    # before step s is waited for, so the lanes do not drain between steps
+    streamed = None
+    if not args.no_stream:
+        sctx = _native.Context(local)
+        slib = sctx.lib
+        sctx.check(slib.of_pairs_open(sctx.handle, H, W, 3, C.byref(P0), args.lanes))
+        souts = [[np.empty((2, H, W), dtype=np.float32) for _ in seeds] for _ in range(2)]
+        spo = [(vp * args.pairs)(*[o.ctypes.data for o in so]) for so in souts]
+
+        def ssubmit(s):
+            t = C.c_int64(0)
+            sctx.check(slib.of_pairs_submit(sctx.handle, args.pairs, p1, p2, spo[s % 2], C.byref(t)))
+            return t.value
+
+        def swait(t0_):
+            for t in range(t0_, t0_ + args.pairs):
+                sctx.check(slib.of_pairs_wait(sctx.handle, t))
+        for s in range(args.warmup):
+            swait(ssubmit(s))
+        barrier(dist)
+        ts = time.perf_counter()
+        prev = ssubmit(0)
+        for s in range(1, args.steps):
+            cur = ssubmit(s)
+            swait(prev)
+            prev = cur
+        swait(prev)
+        barrier(dist)
+        s_elapsed = max_over_ranks(dist, time.perf_counter() - ts)
+        sctx.check(slib.of_pairs_close(sctx.handle))
+        sctx.close()
+        streamed = {"value": round(world * args.pairs * args.steps / s_elapsed, 4),
+                    "ms_per_step": round(1e3 * s_elapsed / args.steps, 3), "steps": args.steps,
+                    "flows_equal_timed": bool(all(np.array_equal(a, b) for a, b in zip(souts[(args.steps - 1) % 2],
+                                                                                        outs))),
+                    "api": "of_pairs_open/submit/wait, step s+1 queued before step s is waited for"}
+
     # device-resident rate: frames uploaded to slots beforehand, flows left in HBM
     for s, (a, b) in enumerate(zip(f1, f2)):
         ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
@@ -547,6 +587,7 @@ def main():
                        "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
                        "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
             "timed_region": "host to host: uint8 RGB pairs in host memory -> flows (fp32) in host memory",
+            "streamed": streamed,
             "device_resident": {"value": round(world * args.pairs * dsteps / dev_elapsed, 4),
                                 "ms_per_step": round(1e3 * dev_elapsed / dsteps, 3), "steps": dsteps,
                                 "host_flow_equals_device_flow": host_eq_dev},

@@ -40,6 +40,7 @@ __device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? l
 struct PenF {
   int kind;
   float p0, p1;
+  double d0, d1;  // the same parameters unrounded (pen_w_f64)
 };
 
 __host__ static inline PenF to_penf(const of_penalty &p) {
@@ -47,6 +48,8 @@ __host__ static inline PenF to_penf(const of_penalty &p) {
   q.kind = p.kind;
   q.p0 = (float)p.p0;
   q.p1 = (float)p.p1;
+  q.d0 = p.p0;
+  q.d1 = p.p1;
   return q;
 }
 
@@ -79,6 +82,36 @@ __device__ __forceinline__ float pen_w(const PenF &p, float x) {
     case OF_PEN_TDIST:
     case OF_PEN_TDIST_UNNORM: return (p.p0 + 1.0f) / (p.p1 * p.p1 * p.p0 + x * x);
     default: return p.p0;  // OF_PEN_CONST
+  }
+}
+
+// rho'(x)/x in fp64 (penalties.py d_type == 2, the reference's own float64
+// formulas): the assembly of ill-conditioned systems (k_flow_operator_f64)
+__device__ __forceinline__ double pen_w_f64(const PenF &p, double x) {
+  switch (p.kind) {
+    case OF_PEN_QUADRATIC: return 2.0 / (p.d0 * p.d0);
+    case OF_PEN_LORENTZIAN: return 2.0 / (2.0 * p.d0 * p.d0 + x * x);
+    case OF_PEN_CHARBONNIER: {
+      const double s2 = p.d0 * p.d0, t = x / s2;
+      return 1.0 / (s2 * sqrt(1.0 + t * t));
+    }
+    case OF_PEN_GEN_CHARBONNIER: return 2.0 * p.d1 * pow(p.d0 * p.d0 + x * x, p.d1 - 1.0);
+    case OF_PEN_GEMAN_MCCLURE: {
+      const double s2 = p.d0 * p.d0, d = s2 + x * x;
+      return 2.0 * s2 / (d * d);
+    }
+    case OF_PEN_HUBER: {
+      const double s2 = p.d0 * p.d0, ax = fabs(x);
+      return ax <= s2 ? 2.0 : 2.0 * s2 / fmax(ax, 1e-300);
+    }
+    case OF_PEN_TUKEY: {
+      const double s2 = p.d0 * p.d0, om = 1.0 - x * x / s2;
+      return fabs(x) <= p.d0 ? 2.0 * om * om / s2 : 0.0;
+    }
+    case OF_PEN_GAUSSIAN: return 1.0 / (p.d0 * p.d0);
+    case OF_PEN_TDIST:
+    case OF_PEN_TDIST_UNNORM: return (p.d0 + 1.0) / (p.d1 * p.d1 * p.d0 + x * x);
+    default: return p.d0;  // OF_PEN_CONST
   }
 }
 

@@ -164,12 +164,18 @@ struct HostStage {
 // k_sor_pipe: persistent grid of one wave per CU; sync words (ticket, fail,
 // stop, counters, decisions, progress stamps) then per-strip partials and the
 // decided sweeps' sums
+// Round-4 A/B on config 2 (tools/ab/r4_sor_ab.sh, the same flow bitwise):
+// publication interval / LDS per wave (waves per CU) / grid cap: 32 / 96 KB
+// (1 per CU) / 256: 7.24 pairs/s; 8 / 96 KB / 256: 9.47; 8 / 32 KB / 512:
+// 12.04; 16 / 32 KB / 512: 10.23; 32 / 32 KB / 512: 7.38.  Several waves per
+// CU let the batch lanes' SOR grids run side by side; a short publication
+// interval lets more sweeps overlap on the 1-2-strip coarse levels.
 #ifndef OF_SOR_PIPE_WAVES
-#define OF_SOR_PIPE_WAVES 256
+#define OF_SOR_PIPE_WAVES 512
 #endif
 // dynamic LDS of a k_sor_pipe wave (unused): bounds the waves per CU
 #ifndef OF_SOR_PIPE_SHM
-#define OF_SOR_PIPE_SHM OF_SOR_SHM
+#define OF_SOR_PIPE_SHM (32 * 1024)
 #endif
 #define OF_SORP_SYNC_BYTES (1024 + SOR_RING_MAX * 2 * SOR_MAXS * sizeof(int))
 #define OF_SORP_BYTES (OF_SORP_SYNC_BYTES + (SOR_RING_MAX * 2 * SOR_MAXS * 2 + SOR_RING_MAX * 2) * sizeof(double))
@@ -590,13 +596,22 @@ OpArgs op_args(const of_params *P, double alpha, double lambda2) {
   o.aq_d = (float)(o.use_r ? alpha : 1.0);
   o.ar_d = (float)(o.use_q ? 1.0 - alpha : 1.0);
   o.lambda2 = (float)lambda2;
+  // AltBA's robust stage (lorentzian + charbonnier(1e-3) coupling) is
+  // ill-conditioned (~3.6e6): its diagonal, a sum of edge weights and a data
+  // term, must be rounded once, not per fp32 operation (k_flow_operator_f64)
+  o.f64 = P->method == OF_METHOD_ALT_BA;
+  o.aq_s_d = (o.use_r ? alpha : 1.0) * P->lambda_q;
+  o.ar_s_d = (o.use_q ? 1.0 - alpha : 1.0) * P->lambda_;
+  o.aq_d_d = o.use_r ? alpha : 1.0;
+  o.ar_d_d = o.use_q ? 1.0 - alpha : 1.0;
+  o.lambda2_d = lambda2;
   return o;
 }
 
 void flow_operator(of_ctx *c, const OpArgs &o, const F2 &uv, const F2 *duv, const Img &It, const Img &Ix,
                    const Img &Iy, const F2 *uvhat, const Img &coef, const F2 &rhs) {
   Grid2 g = grid2(uv.H, uv.W);
-  launch(c, "flow_operator", k_flow_operator, g.grid, g.block, 0, o, (const float2 *)uv.p,
+  launch(c, "flow_operator", o.f64 ? k_flow_operator_f64 : k_flow_operator, g.grid, g.block, 0, o, (const float2 *)uv.p,
          (const float2 *)(duv ? duv->p : nullptr), (const float *)It.p, (const float *)Ix.p, (const float *)Iy.p, It.C,
          (const float2 *)(uvhat ? uvhat->p : nullptr), uv.H, uv.W, uv.P, coef.ps(), coef.p, rhs.p);
 }

@@ -23,6 +23,9 @@ struct OpArgs {
   float aq_d, ar_d;         // data blend: alpha, 1-alpha
   int use_q, use_r;
   float lambda2;            // AltBA coupling weight (0 = off)
+  // k_flow_operator_f64: the blend factors and lambda2 unrounded
+  int f64;
+  double aq_s_d, ar_s_d, aq_d_d, ar_d_d, lambda2_d;
 };
 
 // Per-level derivative planes: for channel c (pointers already offset)

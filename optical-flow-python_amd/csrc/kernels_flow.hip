@@ -217,6 +217,81 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
   }
 }
 
+// The same assembly with every intermediate in fp64 (the reference's own
+// precision) and one rounding per stored plane: for AltBA (OpArgs::f64),
+// whose robust systems are so ill-conditioned that the ~2e-7 relative error
+// of the fp32 assembly's diagonal (a sum of four edge weights, a data term
+// and the coupling) moved the solve by 5x the float32 floor of the system
+// (tools/altba_gpu_probe.py).  Not on the hot path.
+__device__ __forceinline__ double2 edge_w_f64(const OpArgs &o, int axis, double du, double dv) {
+  double wu = 0.0, wv = 0.0;
+  if (o.use_q) { wu += o.aq_s_d * pen_w_f64(o.qsu[axis], du); wv += o.aq_s_d * pen_w_f64(o.qsv[axis], dv); }
+  if (o.use_r) { wu += o.ar_s_d * pen_w_f64(o.rsu[axis], du); wv += o.ar_s_d * pen_w_f64(o.rsv[axis], dv); }
+  return make_double2(wu, wv);
+}
+__device__ __forceinline__ double2 ld_uvd_f64(const float2 *uv, const float2 *duv, size_t k) {
+  const float2 a = uv[k];
+  double2 r = make_double2(a.x, a.y);
+  if (duv) { const float2 b = duv[k]; r.x += b.x; r.y += b.y; }
+  return r;
+}
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator_f64(OpArgs o, const float2 *__restrict__ uv,
+                                const float2 *__restrict__ duv, const float *__restrict__ It,
+                                const float *__restrict__ Ix, const float *__restrict__ Iy, int nc,
+                                const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
+                                float *__restrict__ coef, float2 *__restrict__ rhs) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const double2 c = ld_uvd_f64(uv, duv, k);
+    double2 eR = make_double2(0.0, 0.0), eD = eR, eL = eR, eU = eR;
+    if (j < W - 1) { double2 n = ld_uvd_f64(uv, duv, k + 1); eR = edge_w_f64(o, 0, n.x - c.x, n.y - c.y); }
+    if (i < H - 1) { double2 n = ld_uvd_f64(uv, duv, k + P); eD = edge_w_f64(o, 1, n.x - c.x, n.y - c.y); }
+    if (j > 0) { double2 n = ld_uvd_f64(uv, duv, k - 1); eL = edge_w_f64(o, 0, c.x - n.x, c.y - n.y); }
+    if (i > 0) { double2 n = ld_uvd_f64(uv, duv, k - P); eU = edge_w_f64(o, 1, c.x - n.x, c.y - n.y); }
+    double du = 0.0, dv = 0.0;
+    if (duv) { du = duv[k].x; dv = duv[k].y; }
+    double psq = 0.0, psr = 0.0, ix2 = 0.0, iy2 = 0.0, ixy = 0.0, itx = 0.0, ity = 0.0;
+    for (int ch = 0; ch < nc; ++ch) {
+      const size_t kc = ch * ps + k;
+      const double gx = Ix[kc], gy = Iy[kc], itl = It[kc] + gx * du + gy * dv;
+      if (o.use_q) psq += pen_w_f64(o.qd, itl);
+      if (o.use_r) psr += pen_w_f64(o.rd, itl);
+      ix2 += gx * gx; iy2 += gy * gy; ixy += gx * gy;
+      itx += itl * gx; ity += itl * gy;
+    }
+    const double inv = 1.0 / (double)nc;
+    const double psi = ((o.use_q ? o.aq_d_d * psq : 0.0) + (o.use_r ? o.ar_d_d * psr : 0.0)) * inv;
+    ix2 *= inv; iy2 *= inv; ixy *= inv; itx *= inv; ity *= inv;
+    const float2 u0f = uv[k];
+    const double2 u0 = make_double2(u0f.x, u0f.y);
+    double lu = 0.0, lv = 0.0;
+    if (j < W - 1) { float2 n = uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
+    if (i < H - 1) { float2 n = uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
+    if (j > 0) { float2 n = uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
+    if (i > 0) { float2 n = uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
+    double auu = psi * ix2 + (eL.x + eR.x + eU.x + eD.x);
+    double avv = psi * iy2 + (eL.y + eR.y + eU.y + eD.y);
+    double bu = -lu - psi * itx, bv = -lv - psi * ity;
+    if (uvhat) {  // AltBA coupling (alt_ba.py:236-242)
+      const float2 h = uvhat[k];
+      const double tu = pen_w_f64(o.rc, u0.x - h.x), tv = pen_w_f64(o.rc, u0.y - h.y);
+      auu += o.lambda2_d * tu;
+      avv += o.lambda2_d * tv;
+      bu += o.lambda2_d * tu * (h.x - u0.x);
+      bv += o.lambda2_d * tv * (h.y - u0.y);
+    }
+    coef[k] = (float)eR.x;
+    coef[ps + k] = (float)eD.x;
+    coef[2 * ps + k] = (float)eR.y;
+    coef[3 * ps + k] = (float)eD.y;
+    coef[4 * ps + k] = (float)auu;
+    coef[5 * ps + k] = (float)(psi * ixy);
+    coef[6 * ps + k] = (float)avv;
+    rhs[k] = make_float2((float)bu, (float)bv);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // IRLS update: uv1 = uv + clip(x) (classic_nl.py:250-262); with occ != nullptr
 // also detect_occlusion(uv1, images) (occlusion.py:6-56), where uv1 at the

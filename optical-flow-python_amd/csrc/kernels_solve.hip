@@ -1164,8 +1164,12 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 // launch, wave 3 56 K).  The ring then holds one more row, and wave 0's
 // coefficient loads run one row further ahead (CGS_PF 3) so that a row's
 // load is still two steps from its first use.  Off (0): round 3's layout.
+// Measured (round 4, tools/ab/r4_cgs_ab.sh, 2 reps): 51.1 / 51.7 us per
+// isolated 1080p launch vs 48.9 / 49.2 without, headline 43.76 / 43.69 vs
+// 43.86 / 43.75 pairs/s, the same flow bitwise: wave 0's work does not set
+// the row step alone.  Off by default; kept as an A/B switch.
 #ifndef CGS_REC_SPLIT
-#define CGS_REC_SPLIT (!CGS_PAIR)
+#define CGS_REC_SPLIT 0
 #endif
 #if CGS_REC_SPLIT && CGS_PAIR
 #error "CGS_REC_SPLIT does not form the CGS_PAIR Schur complement"
@@ -1756,12 +1760,17 @@ __global__ __launch_bounds__(256) void k_cg_finalize(float2 *x, const float2 *__
 //     ponged by sweep parity.
 // prefetch distance in steps (<= 7: ring of 8) and steps between progress
 // publications: 7 / 32 vs 4 / 64 = 0.94 vs 1.15 ms per 480x640 sweep, the
-// same iterate (profiles/r3i_sor_ab.log; 16 / 8 steps: 0.89 / 0.91 ms)
+// same iterate (profiles/r3i_sor_ab.log; 16 / 8 steps: 0.89 / 0.91 ms).
+// Round 4: 8 steps (the round-3 note that 8 steps changed the iterate was the
+// compiler contracting the relaxation differently in that build; with
+// sor_relax's explicit fmas every setting gives the same iterate), which lets
+// the pipelined kernel's sweeps trail each other closely (driver.hip
+// OF_SOR_PIPE_WAVES note).
 #ifndef SOR_D
 #define SOR_D 7
 #endif
 #ifndef SOR_G
-#define SOR_G 32
+#define SOR_G 8
 #endif
 #define SOR_MAXS (PCG_MAX_BLOCKS / 2)
 
@@ -1826,6 +1835,12 @@ __device__ __forceinline__ float sor_from_down(float v) {
 // contracted different subsets of the products (the pipelined one packed
 // some into v_pk_mul_f32 + v_add), so their iterates differed in the last
 // bit; spelled out, the rounding is fixed by the source.
+// SOR_RCP: multiply by 1 / a_rr formed at prefetch time instead of dividing
+// on the step's dependency chain (an IEEE division is ~8 dependent
+// instructions); rounds differently from the division (<= 1.5 ulp)
+#ifndef SOR_RCP
+#define SOR_RCP 0
+#endif
 __device__ __forceinline__ float sor_relax(float bb, float wl, float left, float wr, float right, float wd, float down,
                                            float wu, float up, float cc, float other, float dg, float old, float om,
                                            float om1) {
@@ -1834,7 +1849,20 @@ __device__ __forceinline__ float sor_relax(float bb, float wl, float left, float
   sgm = fmaf(wd, down, sgm);
   sgm = fmaf(wu, up, sgm);
   sgm = fmaf(-cc, other, sgm);
+#if SOR_RCP
+  // dg holds 1 / a_rr here (0 where |a_rr| < 1e-15: the row is skipped)
+  return dg == 0.f ? old : fmaf(om1, old, (om * sgm) * dg);
+#else
   return fabsf(dg) < 1e-15f ? old : fmaf(om1, old, (om * sgm) / dg);
+#endif
+}
+// the diagonal as sor_relax takes it
+__device__ __forceinline__ float sor_dg(float a) {
+#if SOR_RCP
+  return fabsf(a) < 1e-15f ? 0.f : 1.0f / a;
+#else
+  return a;
+#endif
 }
 // ||x_new - x_old||^2 and ||x_new||^2 partial sums (fp64)
 __device__ __forceinline__ void sor_acc(float nw, float old, double &dn, double &xn) {
@@ -1880,7 +1908,7 @@ __device__ __forceinline__ void sor_strip(const SorArgs &a, int s, int k, double
     X[q] = ok ? sor_ld(a.x + o) : make_float2(0.f, 0.f);
     WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
     WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
-    DG[q] = ok ? dgp[o] : 0.f;
+    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
     CC[q] = ok ? ccp[o] : 0.f;
     BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
     if (lane == 0) {
@@ -2134,7 +2162,7 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
                    : make_float2(0.f, 0.f);
     WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
     WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
-    DG[q] = ok ? dgp[o] : 0.f;
+    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
     CC[q] = ok ? ccp[o] : 0.f;
     BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
     if (lane == 0) {

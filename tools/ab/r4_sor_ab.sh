@@ -4,8 +4,7 @@
 set -u
 OUT=gpurun_out/r4_sor_ab.log
 : > $OUT
-for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_sor_G8.so tools/ab/lib_sor_G8S32.so \
-         tools/ab/lib_sor_G16S32.so tools/ab/lib_sor_G32S32.so; do
+for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_sor_G4S32.so tools/ab/lib_sor_G8S16.so; do
   echo "== $L" >> $OUT
   OPTFLOW_LIB=$L timeout -k 10 200 python -u bench.py --method hs --solver sor --height 480 --width 640 --steps 2 \
       --warmup 1 --no-profile --no-cpu-baseline > /tmp/b.json 2>&1 || { echo "bench failed $?" >> $OUT; tail -3 /tmp/b.json >> $OUT; exit 1; }
