@@ -1175,6 +1175,24 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #error "CGS_REC_SPLIT does not form the CGS_PAIR Schur complement"
 #endif
 #define CGS_NREC (CGS_REC_SPLIT ? 15 : 14)
+// CGS_RECREG: each wave keeps the coefficient records of the rows it still
+// needs in a register ring and reads only one new record per row step from
+// the LDS ring (wave 0 none: it keeps the records it forms); CGS_RECREG >= 2
+// does the same for the stage rows y (wave 1), g1 (wave 2) and y_q (wave 3).
+// The stages read a record (64 B per lane) and the upper row's vertical
+// weights 9 + 9 times per step otherwise, ~45 KB of a block's ~65 KB of LDS
+// traffic per step.  Measured (profiles/r4e_cgs_recreg_ab.log): isolated
+// 1080p launch 50.1 vs 50.5 us (LDS bandwidth does not bound the step), the
+// timed bench 41.4 vs 44.2 pairs/s: 234 instead of 184 VGPRs leave a SIMD
+// that holds a k_cgs wave room for 2 instead of 3 of the other lanes' waves.
+// The flow also changes in the last bits (the compiler contracts the D^-1
+// products into the consumers once it sees them).  Off.
+#ifndef CGS_RECREG
+#define CGS_RECREG 0
+#endif
+#if CGS_RECREG && CGS_REC_SPLIT
+#error "CGS_RECREG keeps wave 0's own records: not with CGS_REC_SPLIT"
+#endif
 // CGS_E_RAWD: wave 2 loads the raw 2x2 block D (a, c, d planes) of stage E's
 // row itself (L2-resident: wave 0 read it 9 steps earlier) instead of
 // re-forming D from the record's D^-1 (two reciprocals, ~20 VALU per pixel
@@ -1317,6 +1335,16 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
     q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
     q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
+    CgRec r;  // the record as get_rec reads it back
+    r.wx[0] = cg_f2{c.wxu.x, c.wxv.x};
+    r.wy[0] = cg_f2{c.wyu.x, c.wyv.x};
+    r.wx[1] = cg_f2{c.wxu.y, c.wxv.y};
+    r.wy[1] = cg_f2{c.wyu.y, c.wyv.y};
+    r.ma[0] = cg_f2{mi.ia.x, mi.ic.x};
+    r.mb[0] = cg_f2{mi.ic.x, mi.id.x};
+    r.ma[1] = cg_f2{mi.ia.y, mi.ic.y};
+    r.mb[1] = cg_f2{mi.ic.y, mi.id.y};
+    return r;
   };
   // CGS_REC_SPLIT: the record with D still raw (a, c, c, d) in its D^-1 slots
   auto put_raw = [&](int t, const CgRaw &c) {
@@ -1427,10 +1455,11 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     for (int m = 0; m < CGS_W2N; ++m) XI[m] = zero4;
 
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  CgRec QA[2];  // CGS_RECREG: wave 0's records of rows n - 1, n - 2
   if (live) {
     if (role == 0) {
-      put_rec(ns - 2, SGp[0]);
-      put_rec(ns - 1, SGp[1]);
+      QA[0] = put_rec(ns - 2, SGp[0]);  // ring slots of rows ns - 2, ns - 1 at u = 0
+      QA[1] = put_rec(ns - 1, SGp[1]);
       if (CGS_REC_SPLIT) put_raw(ns, SG[0]);  // wave 3 converts it at step ns
     }
     __syncthreads();
@@ -1467,12 +1496,18 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         load_raw(n + CGS_PF, SG[RSG(CGS_PF)]);
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
         RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
+        // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
+#if CGS_RECREG
+        const cg_f2 wu[2] = {QA[R2(-2)].wy[0], QA[R2(-2)].wy[1]};  // before row n takes the slot
+        const CgRec q1 = QA[R2(-1)];
+        QA[R2(0)] = put_rec(n, SG[RSG(0)]);
+#else
         if (CGS_REC_SPLIT) put_raw(n + 1, SG[RSG(1)]);
         else put_rec(n, SG[RSG(0)]);
-        // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
         const CgRec q1 = get_rec(n - 1);
         cg_f2 wu[2];
         get_wy(n - 2, wu);
+#endif
         cg_f4 r = RI[RRI(-1)];
         if (!FIRST) r -= alpha * (cgr_diag_raw(SG[RSG(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
         const cg_f4 y = cgr_pinv(q1, r);
@@ -1493,49 +1528,94 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         const float4 a = s_y[t & 7][lane];
         return cg_f4{a.x, a.y, a.z, a.w};
       };
+#if CGS_RECREG
+      CgRec QB[4];  // records of rows n - 3 .. n - 6 (rows above the band: zero, as in LDS)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) QB[m] = CgRec{};
+#define CGS_REC1(d) QB[R4(d)]
+#define CGS_WY1(d, w) const cg_f2 w[2] = {QB[R4(d)].wy[0], QB[R4(d)].wy[1]}
+#else
+#define CGS_REC1(d) get_rec(n + (d))
+#define CGS_WY1(d, w) \
+  cg_f2 w[2];         \
+  get_wy(n + (d), w)
+#endif
+#if CGS_RECREG >= 2
+      cg_f4 Y1[8] = {zero4, zero4, zero4, zero4, zero4, zero4, zero4, zero4};  // y rows n-2 .. n-6
+#define CGS_Y1(d) Y1[R8(d)]
+#else
+#define CGS_Y1(d) yrow(n + (d))
+#endif
       CGS_STEPS({
+#if CGS_RECREG >= 2
+        Y1[R8(-2)] = yrow(n - 2);
+#endif
+#if CGS_RECREG
+        CGS_WY1(-7, w7);  // row n-7's vertical weights, before row n-3 takes its slot
+        QB[R4(-3)] = get_rec(n - 3);
+#else
+        CGS_WY1(-7, w7);
+#endif
         {
-          const CgRec q = get_rec(n - 3);
-          cg_f2 wu[2];
-          get_wy(n - 4, wu);
-          const cg_f4 y0 = yrow(n - 3);
-          const cg_f4 ny = cgr_nsum_p(yrow(n - 4), y0, yrow(n - 2), q, wu);
+          const CgRec q = CGS_REC1(-3);
+          CGS_WY1(-4, wu);
+          const cg_f4 y0 = CGS_Y1(-3);
+          const cg_f4 ny = cgr_nsum_p(CGS_Y1(-4), y0, CGS_Y1(-2), q, wu);
           G4[R4(-3)] = c4 * y0 + c5 * cgr_pinv(q, ny);
         }
         {
-          const CgRec q = get_rec(n - 4);
-          cg_f2 wu[2];
-          get_wy(n - 5, wu);
+          const CgRec q = CGS_REC1(-4);
+          CGS_WY1(-5, wu);
           const cg_f4 ng = cgr_nsum_p(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
-          G3[R4(-4)] = c3 * yrow(n - 4) + cgr_pinv(q, ng);
+          G3[R4(-4)] = c3 * CGS_Y1(-4) + cgr_pinv(q, ng);
         }
         {
-          const CgRec q = get_rec(n - 5);
-          cg_f2 wu[2];
-          get_wy(n - 6, wu);
+          const CgRec q = CGS_REC1(-5);
+          CGS_WY1(-6, wu);
           const cg_f4 ng = cgr_nsum_p(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
-          G2[R4(-5)] = c2 * yrow(n - 5) + cgr_pinv(q, ng);
+          G2[R4(-5)] = c2 * CGS_Y1(-5) + cgr_pinv(q, ng);
         }
         {
-          const CgRec q = get_rec(n - 6);
-          cg_f2 wu[2];
-          get_wy(n - 7, wu);
-          const cg_f4 ng = cgr_nsum_p(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, wu);
-          st4(s_g1, n - 6, c1 * yrow(n - 6) + cgr_pinv(q, ng));
+          const CgRec q = CGS_REC1(-6);
+          const cg_f4 ng = cgr_nsum_p(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, w7);
+          st4(s_g1, n - 6, c1 * CGS_Y1(-6) + cgr_pinv(q, ng));
         }
       })
+#undef CGS_REC1
+#undef CGS_WY1
+#undef CGS_Y1
     } else if (role == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
+#if CGS_RECREG
+      CgRec QC[2] = {CgRec{}, CgRec{}};  // records of rows n - 8, n - 9
+#endif
+#if CGS_RECREG >= 2
+      cg_f4 G1[4] = {zero4, zero4, zero4, zero4};  // g1 rows n-7 .. n-9
+#endif
       CGS_STEPS({
+#if CGS_RECREG
+        const cg_f2 w10[2] = {QC[R2(-10)].wy[0], QC[R2(-10)].wy[1]};  // before row n-8 takes the slot
+        QC[R2(-8)] = get_rec(n - 8);
+#endif
         PO2[RW2(CGS_PF2 - 8)] = load_po(n + CGS_PF2 - 8);
         XI[RW2(CGS_PF2 - 8)] = load_x(n + CGS_PF2 - 8);
         if (CGS_E_RAWD) load_acd(n + CGS_PF2 - 9, RD[RW2(CGS_PF2 - 9)]);
         // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
+#if CGS_RECREG
+          const CgRec q4 = QC[R2(-8)];
+          const cg_f2 wu[2] = {QC[R2(-9)].wy[0], QC[R2(-9)].wy[1]};
+#else
           const CgRec q4 = get_rec(n - 8);
           cg_f2 wu[2];
           get_wy(n - 9, wu);
+#endif
+#if CGS_RECREG >= 2
+          G1[R4(-7)] = ld4(s_g1, n - 7);
+          const cg_f4 ng = cgr_nsum_p(G1[R4(-9)], G1[R4(-8)], G1[R4(-7)], q4, wu);
+#else
           const cg_f4 ng = cgr_nsum_p(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
+#endif
           const float4 b = s_y[(n - 8) & 7][lane];
           const cg_f4 yr = {b.x, b.y, b.z, b.w};
           const cg_f4 z = c0 * yr + cgr_pinv(q4, ng);
@@ -1555,9 +1635,14 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         }
         // E) row n-9: q = A p, y_q = D^-1 q
         {
+#if CGS_RECREG
+          const CgRec q5 = QC[R2(-9)];
+          const cg_f2(&wu)[2] = w10;
+#else
           const CgRec q5 = get_rec(n - 9);
           cg_f2 wu[2];
           get_wy(n - 10, wu);
+#endif
           const cg_f4 pm = PP[R4(-9)];
           const cg_f4 q = (CGS_E_RAWD ? cgr_diag_raw(RD[RW2(-9)], pm) : cgr_diag_p(q5, pm)) -
                           cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
@@ -1577,16 +1662,37 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       // T5 = v2.N v2 (row n-12; T5 counts each edge once, by its right /
       // lower pixel)
       cg_f4 V1[4] = {zero4, zero4, zero4, zero4}, V2[2] = {zero4, zero4};
+#if CGS_RECREG
+      CgRec QD[2] = {CgRec{}, CgRec{}};  // records of rows n - 11, n - 12
+#endif
+#if CGS_RECREG >= 2
+      cg_f4 YQ[4] = {zero4, zero4, zero4, zero4};  // y_q rows n-10 .. n-12
+#endif
       CGS_STEPS({
+#if CGS_RECREG
+        const cg_f2 w13[2] = {QD[R2(-13)].wy[0], QD[R2(-13)].wy[1]};  // before row n-11 takes the slot
+        QD[R2(-11)] = get_rec(n - 11);
+#endif
         // row n's record: raw since wave 0 stored it at step n - 1; stage A
         // reads it at step n + 1
         if (CGS_REC_SPLIT) convert_rec(n);
         {
+#if CGS_RECREG
+          const CgRec q6 = QD[R2(-11)];
+          const cg_f2 wu[2] = {QD[R2(-12)].wy[0], QD[R2(-12)].wy[1]};
+#else
           const CgRec q6 = get_rec(n - 11);
           cg_f2 wu[2];
           get_wy(n - 12, wu);
+#endif
+#if CGS_RECREG >= 2
+          YQ[R4(-10)] = ld4(s_yq, n - 10);
+          const cg_f4 yq = YQ[R4(-11)];
+          const cg_f4 ny = cgr_nsum_p(YQ[R4(-12)], yq, YQ[R4(-10)], q6, wu);
+#else
           const cg_f4 yq = ld4(s_yq, n - 11);
           const cg_f4 ny = cgr_nsum_p(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
+#endif
           const cg_f4 v1 = cgr_pinv(q6, ny);
           V1[R4(-11)] = v1;
           const int o = n - 11;
@@ -1596,9 +1702,14 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           }
         }
         {
+#if CGS_RECREG
+          const CgRec q7 = QD[R2(-12)];
+          const cg_f2(&wy7)[2] = w13;
+#else
           const CgRec q7 = get_rec(n - 12);
           cg_f2 wy7[2];
           get_wy(n - 13, wy7);
+#endif
           const cg_f4 v1 = V1[R4(-12)];
           const cg_f4 nv = cgr_nsum_p(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
           const cg_f4 v2 = cgr_pinv(q7, nv);
