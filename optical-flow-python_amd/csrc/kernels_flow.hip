@@ -470,6 +470,12 @@ extern __device__ unsigned long long g_wmf_t[];
 #define WMF_STAMP(i)
 #endif
 #define WMF_NC 8
+// WMF_CID_PAIR: the u- and v-list chunk ids of a region sample side by side
+// ([RW][RP][2] u8, one u16 read per window sample) instead of two planes
+// ([2][RW][RP] u8, two u8 reads)
+#ifndef WMF_CID_PAIR
+#define WMF_CID_PAIR 0
+#endif
 // chunk-sum type: fp64 (default, 100 % exact on every fixture) or fp32
 // (WMF_F32SUM: half the chunk-sum LDS).  The fp32 build emits native
 // ds_add_f32 (checked in the ISA, no CAS loop) and yet runs 4.93 vs 0.83 ms
@@ -677,8 +683,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const unsigned pa = (uint16_t)a[r], pb = (uint16_t)b[r];
     ku[e] = (uint16_t)pa;  // padding keys -> 0xffff: out of every window
     kv[e] = (uint16_t)pb;
-    if (pa != 0xffffu) cid[2 * ((pa >> 8) * RP + (pa & 0xffu))] = (uint8_t)(e / CH);
-    if (pb != 0xffffu) cid[2 * ((pb >> 8) * RP + (pb & 0xffu)) + 1] = (uint8_t)(e / CH);
+    const int qa = (pa >> 8) * RP + (pa & 0xffu), qb_ = (pb >> 8) * RP + (pb & 0xffu);
+    if (pa != 0xffffu) cid[WMF_CID_PAIR ? 2 * qa : qa] = (uint8_t)(e / CH);
+    if (pb != 0xffffu) cid[WMF_CID_PAIR ? 2 * qb_ + 1 : RW * RP + qb_] = (uint8_t)(e / CH);
   }
   __syncthreads();
   WMF_STAMP(2);
@@ -705,9 +712,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     for (int dx = 0; dx < MX; ++dx)
       if (dx < n) {
         rec[dx] = smp[q0 + dx];
-        const unsigned pr = reinterpret_cast<const uint16_t *>(cid)[q0 + dx];
-        cu[dx] = pr & 0xffu;
-        cv[dx] = pr >> 8;
+        if (WMF_CID_PAIR) {
+          const unsigned pr = reinterpret_cast<const uint16_t *>(cid)[q0 + dx];
+          cu[dx] = pr & 0xffu;
+          cv[dx] = pr >> 8;
+        } else {
+          cu[dx] = cid[q0 + dx];
+          cv[dx] = cid[RW * RP + q0 + dx];
+        }
       }
 #pragma unroll
     for (int dx = 0; dx < MX; ++dx)

@@ -146,12 +146,15 @@ class PairStream:
         self._live[t.value] = (a, b, out)
         return t.value
 
-    def wait(self, ticket):
-        """Block until the pair's flow is ready; (H, W, 2) float64."""
+    def wait(self, ticket, planar=False):
+        """Block until the pair's flow is ready; (H, W, 2) float64, or with
+        `planar` the library's (2, H, W) float32 planes as they came back (the
+        conversion can then run on another thread)."""
         if ticket not in self._live:
             raise ValueError(f"unknown or already waited ticket {ticket}")
         self._ctx.check(self._ctx.lib.of_pairs_wait(self._ctx.handle, int(ticket)))
-        return nat.interleaved(self._live.pop(ticket)[2])
+        out = self._live.pop(ticket)[2]
+        return out if planar else nat.interleaved(out)
 
     def close(self):
         if self._ctx is not None:

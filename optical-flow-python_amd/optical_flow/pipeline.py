@@ -4,25 +4,28 @@ The steps either side of `estimate_flow` in a benchmark run of the reference
 (its notebooks loop over them one pair at a time): PNG decode in
 `read_flow_file`'s layout (`flo_io.py:66-113`) -> flow -> `write_flo`
 (`flo_io.py:46-63`) + `flow_angular_error` against the ground truth when one
-exists (`metrics.py:5-53`).  Here the flows of a chunk of same-size pairs come
-from ONE `of_pairs_run_host` call (`estimate_flow_batch`: `lanes` pairs in
-flight, H2D/D2H overlapped inside the library), and the host file work is
-overlapped with the GPU:
+exists (`metrics.py:5-53`).  Here every decoded pair goes into a PairStream
+(`of_pairs_open` / `of_pairs_submit` / `of_pairs_wait`: `lanes` GPU pipelines
+fed from a queue, H2D/D2H overlapped inside the library), kept open between
+calls, and the host file work is overlapped with the GPU:
 
-    decode pool   : chunk j+1's PNGs (+ GT .flo)                  \
-    this thread   : chunk j on the GPU (ctypes releases the GIL)   } at once
-    writer pool   : chunk j-1's .flo files + AAE/AEPE              /
+    decode pool   : the next pairs' PNGs (+ GT .flo)              \
+    this thread   : submits decoded pairs, waits for the oldest    } at once
+    writer pool   : .flo files + AAE/AEPE from the flow planes      /
 
+(`stream=False`: the round-3 form, chunks of same-size pairs per
+`of_pairs_run_host` call, which drains the lanes at every chunk boundary.)
 Pairs are grouped by frame shape (Middlebury sequences differ in size) and
 results come back in job order.  Each flow equals `estimate_flow(im1, im2,
 method, params)` on the decoded frames: bitwise below 2^20 px, and to CG
 rounding at >= 2^20 px with lanes >= 2, where two pairs' fine solves run side
 by side in another block geometry (include/optflow.h, of_pairs_run).
 """
+import atexit
 import os
 import threading
 import time
-from collections import namedtuple
+from collections import OrderedDict, namedtuple
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -55,36 +58,51 @@ def middlebury_jobs(data_dir, seqs=None, i_seq=10, out_dir=None):
     return jobs
 
 
-def decode_pair(job):
-    """(uint8 frame 1, uint8 frame 2, ground truth (H, W, 2) float32 or None).
-    RGB(A) PNGs keep their first 3 channels (estimate_flow uses im[:, :, :3])."""
+def load_frame(p):
+    """One 8-bit PNG frame as uint8; RGB(A) keeps its first 3 channels
+    (estimate_flow uses im[:, :, :3])."""
     from PIL import Image
+    a = np.asarray(Image.open(p))
+    if a.dtype != np.uint8:
+        raise ValueError(f"{p}: {a.dtype} frames are not supported (8-bit PNGs only)")
+    if a.ndim == 3:
+        if a.shape[2] < 3:
+            raise ValueError(f"{p}: {a.shape[2]}-channel frames are not supported")
+        a = a[:, :, :3]
+    return np.ascontiguousarray(a)
 
-    def load(p):
-        a = np.asarray(Image.open(p))
-        if a.dtype != np.uint8:
-            raise ValueError(f"{p}: {a.dtype} frames are not supported (8-bit PNGs only)")
-        if a.ndim == 3:
-            if a.shape[2] < 3:
-                raise ValueError(f"{p}: {a.shape[2]}-channel frames are not supported")
-            a = a[:, :, :3]
-        return np.ascontiguousarray(a)
 
-    a, b = load(job.im1), load(job.im2)
+def _pair_of(job, a, b, gt):
     if a.shape != b.shape:
         raise ValueError(f"{job.name}: frame shapes differ {a.shape} vs {b.shape}")
-    return a, b, (read_flo(job.gt) if job.gt else None)
+    return a, b, gt
 
 
-def _finish(job, uv, gt, border):
-    """Write the .flo and evaluate one pair (writer thread)."""
-    res = {"name": job.name, "shape": uv.shape[:2], "out": job.out}
+def decode_pair(job):
+    """(uint8 frame 1, uint8 frame 2, ground truth (H, W, 2) float32 or None)."""
+    return _pair_of(job, load_frame(job.im1), load_frame(job.im2), read_flo(job.gt) if job.gt else None)
+
+
+def _finish(job, uv, gt, border, keep=False):
+    """Write the .flo and evaluate one pair (writer thread).  `uv` (H, W, 2),
+    or the library's (2, H, W) float32 planes (PairStream.wait(planar=True)):
+    then the .flo is written from the planes and the metrics take them as
+    they are (flow_angular_error computes in float64 either way, so the
+    numbers are the same), and only `keep` builds the (H, W, 2) float64 flow."""
+    planar = uv.ndim == 3 and uv.shape[0] == 2 and uv.dtype == np.float32
+    u, v = (uv[0], uv[1]) if planar else (uv[..., 0], uv[..., 1])
+    res = {"name": job.name, "shape": u.shape, "out": job.out}
     if job.out:
         os.makedirs(os.path.dirname(os.path.abspath(job.out)), exist_ok=True)
-        write_flo(uv, job.out)
+        write_flo(np.moveaxis(uv, 0, 2) if planar else uv, job.out)
     if gt is not None:
-        aae, std, aepe = flow_angular_error(gt[..., 0], gt[..., 1], uv[..., 0], uv[..., 1], border)
+        aae, std, aepe = flow_angular_error(gt[..., 0], gt[..., 1], u, v, border)
         res.update(aae=float(aae), std_ae=float(std), aepe=float(aepe))
+    if keep:
+        if planar:
+            from optical_flow import _native as nat
+            uv = nat.interleaved(uv)
+        res["uv"] = uv
     return res
 
 
@@ -170,10 +188,35 @@ def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, 
     return results, stats
 
 
-def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, border, keep_flows, max_streams=2):
+# Open PairStreams kept between run_pipeline calls (a server's pool: lane
+# threads, contexts and arenas stay warm), keyed by (frame shape, method,
+# params, lanes); at most _MAX_STREAMS, the least recently used closed first.
+_STREAMS = OrderedDict()
+_MAX_STREAMS = 2
+_STREAMS_LOCK = threading.Lock()
+
+
+def close_streams():
+    """Close every PairStream run_pipeline keeps open (frees their lanes'
+    device memory); the next run_pipeline call opens new ones."""
+    with _STREAMS_LOCK:
+        while _STREAMS:
+            _STREAMS.popitem(last=False)[1].close()
+
+
+atexit.register(close_streams)
+
+
+def _stream_key(shape, method, params, lanes):
+    return (shape, method, repr(sorted(params.items())) if isinstance(params, dict) else repr(params), lanes)
+
+
+def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, border, keep_flows,
+                   max_streams=_MAX_STREAMS):
     """run_pipeline's streaming form: decode pool -> PairStream per frame
-    shape (at most `max_streams` open; the least recently used one is drained
-    and closed) -> writer pool, results in job order."""
+    shape (kept open in _STREAMS for later calls; at most `max_streams`, the
+    least recently used one drained and closed) -> writer pool, results in job
+    order."""
     from optical_flow.interface import PairStream
     t_start = time.perf_counter()
     lock = threading.Lock()
@@ -187,8 +230,8 @@ def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, 
             with lock:
                 busy[key] += time.perf_counter() - t0
 
-    streams = {}    # shape -> PairStream, in least-recently-used order
-    inflight = {}   # shape -> [(job index, ticket, ground truth)]
+    streams = _STREAMS   # key -> PairStream, least recently used first
+    inflight = {}   # key -> [(job index, ticket, ground truth)]
     window = 2 * lanes + 2
     results = [None] * len(jobs)
     writes = []
@@ -198,47 +241,55 @@ def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, 
         ahead = 2 * max(1, ahead_chunks)
 
         def submit_upto(n):
+            # the two frames and the GT of a pair decode on separate workers
+            # (the first pair's decode is the pipeline's start-up latency)
             nonlocal nsub
             while nsub < min(n, len(jobs)):
-                futs[nsub] = dec.submit(timed, "decode_s", decode_pair, jobs[nsub])
+                j = jobs[nsub]
+                futs[nsub] = (dec.submit(timed, "decode_s", load_frame, j.im1),
+                              dec.submit(timed, "decode_s", load_frame, j.im2),
+                              dec.submit(timed, "decode_s", read_flo, j.gt) if j.gt else None)
                 nsub += 1
 
-        def retire(shape):
-            i, t, gt = inflight[shape].pop(0)
-            uv = timed("gpu_s", streams[shape].wait, t)
-            writes.append((i, wr.submit(timed, "write_s", _finish, jobs[i], uv, gt, border), uv if keep_flows else None))
+        def retire(key):
+            i, t, gt = inflight[key].pop(0)
+            uv = timed("gpu_s", streams[key].wait, t, True)  # planar: converted by the writer
+            writes.append((i, wr.submit(timed, "write_s", _finish, jobs[i], uv, gt, border, keep_flows)))
 
-        def close(shape):
-            while inflight[shape]:
-                retire(shape)
-            streams.pop(shape).close()
-            del inflight[shape]
+        def drain(key):
+            while inflight.get(key):
+                retire(key)
+            inflight.pop(key, None)
 
-        try:
-            for i in range(len(jobs)):
-                submit_upto(i + ahead)
-                a, b, gt = futs[i].result()
-                futs[i] = None
-                shape = a.shape
-                if shape not in streams:
-                    if len(streams) >= max_streams:
-                        close(next(iter(streams)))
-                    streams[shape] = PairStream(shape[0], shape[1], 3 if a.ndim == 3 else 1, method, params, lanes)
-                    inflight[shape] = []
-                else:
-                    streams[shape] = streams.pop(shape)  # most recently used last
-                inflight[shape].append((i, streams[shape].submit(a, b), gt))
-                while len(inflight[shape]) > window:
-                    retire(shape)
-            for shape in list(streams):
-                close(shape)
-        finally:
-            for st in streams.values():
-                st.close()
-        for i, f, uv in writes:
+        with _STREAMS_LOCK:
+            try:
+                for i in range(len(jobs)):
+                    submit_upto(i + ahead)
+                    fa, fb, fg = futs[i]
+                    futs[i] = None
+                    a, b, gt = _pair_of(jobs[i], fa.result(), fb.result(), fg.result() if fg else None)
+                    key = _stream_key(a.shape, method, params, lanes)
+                    if key not in streams:
+                        while len(streams) >= max_streams:
+                            old = next(iter(streams))
+                            drain(old)
+                            streams.pop(old).close()
+                        streams[key] = PairStream(a.shape[0], a.shape[1], 3 if a.ndim == 3 else 1, method,
+                                                  params, lanes)
+                    streams.move_to_end(key)  # most recently used last
+                    inflight.setdefault(key, []).append((i, streams[key].submit(a, b), gt))
+                    while len(inflight[key]) > window:
+                        retire(key)
+                for key in list(inflight):
+                    drain(key)
+            except BaseException:
+                # a failed run leaves no half-drained stream behind
+                for key in list(inflight):
+                    if key in streams:
+                        streams.pop(key).close()
+                raise
+        for i, f in writes:
             results[i] = f.result()
-            if keep_flows:
-                results[i]["uv"] = uv
     wall = time.perf_counter() - t_start
     stats = {"pairs": len(jobs), "wall_s": wall, "pairs_per_s": len(jobs) / wall if wall > 0 else 0.0,
              "stream": True}

@@ -130,6 +130,16 @@ def test_pipeline_gpu_matches_estimate_flow(tmp_path, stream):
     rw = res[0]
     print(f"RubberWhale AAE {rw['aae']:.5f} AEPE {rw['aepe']:.6f} (reference 2.46298 / 0.080250)")
     assert abs(rw["aepe"] - 0.080250) <= 1e-3 and abs(rw["aae"] - 2.46298) <= 0.02
+    if stream:
+        # the streams stay open for the next call (at most two), which gives
+        # the same flows; close_streams releases them
+        from optical_flow import pipeline as pl
+        assert 1 <= len(pl._STREAMS) <= 2
+        res2, _ = run_pipeline(jobs, lanes=3, chunk=2, keep_flows=True)
+        for r, q in zip(res, res2):
+            np.testing.assert_array_equal(r["uv"], q["uv"])
+        pl.close_streams()
+        assert not pl._STREAMS
 
 
 @pytest.mark.gpu

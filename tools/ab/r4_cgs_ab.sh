@@ -13,6 +13,6 @@ for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_cg
     OPTFLOW_LIB=$L timeout -k 10 120 python -u tools/ab/bitwise.py 540 960 >> $OUT 2>&1 || exit 1
   fi
   OPTFLOW_LIB=$L timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-profile --no-cpu-baseline > /tmp/b.json 2>&1 || { tail -3 /tmp/b.json >> $OUT; exit 1; }
-  python3 -c "import json; d=json.loads(open('/tmp/b.json').read().strip().splitlines()[-1]); print('headline pairs/s', d['value'], 'dev', d['device_resident']['value'])" >> $OUT
+  python3 -c "import json; d=json.loads(open('/tmp/b.json').read().strip().splitlines()[-1]); print('headline pairs/s', d['value'], 'host', d['host_to_host']['value'])" >> $OUT
 done
 done
