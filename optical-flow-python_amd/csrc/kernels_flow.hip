@@ -506,6 +506,28 @@ struct WmfRec<1> {
 
 typedef float wmf_v2f __attribute__((ext_vector_type(2)));
 
+// WMF_SHIFT: in the window pass (compile-time window), lane px of a tile row
+// takes region column px + dx from lane px + 1's column of the previous step
+// (DPP row_shl:1) instead of reading it from LDS again; only the last lane of
+// each 8-lane tile row (px = 7, lanes 7 / 15 of a 16-lane DPP row) reads the
+// new column.  The same records in the same order: bitwise the same sums.
+// Measured (profiles/r4j_wmf_shift_ab.log): 0.918 vs 0.771 ms per 1080p
+// launch — the 5 DPP moves + select per sample cost more VALU than the LDS
+// reads they save; the pass is VALU / latency bound, not LDS bound.  Off.
+#ifndef WMF_SHIFT
+#define WMF_SHIFT 0
+#endif
+__device__ __forceinline__ float wmf_shl1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x101, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float4 wmf_shl1(const float4 &v) {
+  return make_float4(wmf_shl1(v.x), wmf_shl1(v.y), wmf_shl1(v.z), wmf_shl1(v.w));
+}
+__device__ __forceinline__ float2 wmf_shl1(const float2 &v) { return make_float2(wmf_shl1(v.x), wmf_shl1(v.y)); }
+__device__ __forceinline__ unsigned wmf_shl1(unsigned v) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, true);
+}
+
 // weight of region sample s for a pixel of guide colour (c01, c2):
 // max(2^(nk |dlab|^2) occ, 1e-10), channels 0-1 in packed fp32.  Called from
 // the window pass and the chunk walk: both must round identically, so no
@@ -729,7 +751,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
       }
   };
-  if (HS > 0) {
+  // WMF_SHIFT form of visit_row (compile-time window only)
+  auto visit_row_shift = [&](int q0) {
+    constexpr int MX = 2 * HS + 1;
+    const bool edge = px == 7;
+    auto ids = [&](int q) {
+      if (WMF_CID_PAIR) return (unsigned)reinterpret_cast<const uint16_t *>(cid)[q];
+      return (unsigned)cid[q] | ((unsigned)cid[RW * RP + q] << 8);
+    };
+    T ext[MX > 1 ? MX : 2];
+    unsigned eid[MX > 1 ? MX : 2];
+#pragma unroll
+    for (int dx = 1; dx < MX; ++dx)
+      if (edge) {
+        ext[dx] = smp[q0 + dx];
+        eid[dx] = ids(q0 + dx);
+      }
+    T cur = smp[q0];
+    unsigned id = ids(q0);
+#pragma unroll
+    for (int dx = 0; dx < MX; ++dx) {
+      if (dx > 0) {
+        cur = wmf_shl1(cur);
+        id = wmf_shl1(id);
+        if (edge) {
+          cur = ext[dx];
+          id = eid[dx];
+        }
+      }
+      const wmf_sum_t w = (wmf_sum_t)wmf_w(cur, c01, cg[2], nk);
+      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + ((id & 0xffu) << WMF_SUM_SHIFT)), w);
+      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + ((id >> 8) << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
+    }
+  };
+  if (HS > 0 && WMF_SHIFT) {
+#pragma unroll
+    for (int dy = 0; dy <= 2 * HS; ++dy) visit_row_shift(qb + dy * RP);
+  } else if (HS > 0) {
 #pragma unroll
     for (int dy = 0; dy <= 2 * HS; ++dy) visit_row(qb + dy * RP, 2 * HS + 1);
   } else {

@@ -30,8 +30,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--chunk", type=int, default=8)
-    ap.add_argument("--workers", type=int, default=6)
-    ap.add_argument("--writers", type=int, default=5)
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--writers", type=int, default=4)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     tmp = a.out or tempfile.mkdtemp(prefix="ofpipe_")
