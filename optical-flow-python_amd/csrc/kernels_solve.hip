@@ -1190,6 +1190,10 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #ifndef CGS_RECREG
 #define CGS_RECREG 0
 #endif
+// CGS_PRIO_ALL: waves 1 and 3 at issue priority 1 (0 otherwise)
+#ifndef CGS_PRIO_ALL
+#define CGS_PRIO_ALL 0
+#endif
 #if CGS_RECREG && CGS_REC_SPLIT
 #error "CGS_RECREG keeps wave 0's own records: not with CGS_REC_SPLIT"
 #endif
@@ -1469,6 +1473,11 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     // per 1080p launch (A/B, profiles/r2z_cgs_setprio_ab.log; wave 0
     // alone: 51.3)
     if (role == 0 || role == 2) __builtin_amdgcn_s_setprio(2);
+#if CGS_PRIO_ALL
+    // the Horner and T waves above other kernels' waves on their SIMD (the
+    // timed lanes run a fine solve one block per CU beside other lanes' work)
+    else __builtin_amdgcn_s_setprio(1);
+#endif
     // each wave runs its own role's loop (registers of one role only), one
     // block barrier per row step in every role (same step count)
 #define CGS_STEPS(...)                                                    \
