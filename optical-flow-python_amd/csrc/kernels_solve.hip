@@ -1190,9 +1190,13 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #ifndef CGS_RECREG
 #define CGS_RECREG 0
 #endif
-// CGS_PRIO_ALL: waves 1 and 3 at issue priority 1 (0 otherwise)
+// CGS_PRIO_ALL: waves 1 and 3 at issue priority 1 (0 otherwise), above the
+// other lanes' kernels that share their SIMDs in the timed geometry: 45.65 /
+// 45.78 / 45.87 vs 45.34 / 45.45 / 45.57 pairs/s, 3 reps each
+// (profiles/r4k_prio_ab.log); the same arithmetic
+
 #ifndef CGS_PRIO_ALL
-#define CGS_PRIO_ALL 0
+#define CGS_PRIO_ALL 1
 #endif
 #if CGS_RECREG && CGS_REC_SPLIT
 #error "CGS_RECREG keeps wave 0's own records: not with CGS_REC_SPLIT"
