@@ -133,6 +133,7 @@ template <int INTERP>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H,
                                                                 int W, int P, size_t ps, float *__restrict__ It,
                                                                 float *__restrict__ Ix, float *__restrict__ Iy) {
+  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
                                 const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
                                 int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
+  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -305,6 +307,7 @@ __device__ __forceinline__ float2 upd(const float2 *uv, const float2 *x, size_t 
 __global__ void k_update_occ(const float2 *__restrict__ uv, const float2 *__restrict__ x, int clip,
                              float2 *__restrict__ uv1, const float *__restrict__ I1, const float *__restrict__ I2,
                              int nc, float *__restrict__ occ, int H, int W, int P, size_t ps) {
+  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -651,6 +654,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
                                              int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt,
                                              const float2 *base) {
   using T = typename WmfRec<GC>::T;
+  OF_PRIO_WMF();
   constexpr int N = NPER * 64, CH = N / WMF_NC;
   const int hsz = HS > 0 ? HS : hsz_rt;
   // region width and record pitch: compile-time with HS (no runtime divides)

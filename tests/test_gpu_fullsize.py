@@ -150,3 +150,33 @@ def test_fullsize_1080_timed_geometry():
     assert abs(a_gpu - a_ref) <= 1e-3
     g_mean, g_med, g_p99 = CASES["cfg4_classic_nl_fast_1080"][-1]
     assert s["mean"] <= g_mean and s["median"] <= g_med and s["p99"] <= g_p99, s
+
+
+def test_fullsize_4k_largest_frame():
+    """The largest frame size exercised (2160x3840, 4x config 4's pixels): the
+    pyramid depth, the k_cgs band geometry (single solve and the lanes
+    mode's side-by-side fine solves) and the arena sizing at 8.3 Mpx.  No
+    reference run exists at this size (the reference needs hours per 1080p
+    pair), so the checks are size-independent properties: every solve's fp64
+    true residual within 1.5x the surrogate's rtol, the AEPE against the
+    analytic ground truth of the same order as at 1080p (0.0526 there), and
+    a 2-lane batch of the pair equal to estimate_flow to CG rounding."""
+    import optical_flow
+    from optical_flow.utils.synthetic import synth_pair
+    uv, gt, recs = _run("classic+nl-fast", None, 2160, 3840, log=True)
+    assert uv.shape == (2160, 3840, 2) and np.all(np.isfinite(uv))
+    assert len(recs) >= 27, len(recs)
+    assert all(r["done"] in (1, 3) for r in recs), [r for r in recs if r["done"] not in (1, 3)]
+    worst = max(r["true_rel"] for r in recs)
+    a = _aepe(uv, gt)
+    print(f"4k: {len(recs)} solves, worst true residual {worst:.3e}, AEPE {a:.5f}")
+    assert worst <= 1.5e-6, worst
+    assert a <= 0.15, a
+    im1, im2, _ = synth_pair(2160, 3840, 0)
+    f = optical_flow.estimate_flow_batch([im1.astype(np.uint8)] * 2, [im2.astype(np.uint8)] * 2,
+                                         "classic+nl-fast", lanes=2)
+    for x in f:
+        s = epe_stats(x, uv)
+        print(f"4k batch vs estimate_flow: {s}")
+        assert s["mean"] <= 1e-4, s
+    np.testing.assert_array_equal(f[0], f[1])
