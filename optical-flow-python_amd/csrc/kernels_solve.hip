@@ -1198,8 +1198,24 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 #ifndef CGS_PRIO_ALL
 #define CGS_PRIO_ALL 1
 #endif
-#if CGS_RECREG && CGS_REC_SPLIT
-#error "CGS_RECREG keeps wave 0's own records: not with CGS_REC_SPLIT"
+// per-wave form (A/B): CGS_RR<role> = 1 gives that wave its register ring
+#ifndef CGS_RR0
+#define CGS_RR0 (CGS_RECREG != 0)
+#endif
+#ifndef CGS_RR1
+#define CGS_RR1 (CGS_RECREG != 0)
+#endif
+#ifndef CGS_RR2
+#define CGS_RR2 (CGS_RECREG != 0)
+#endif
+#ifndef CGS_RR3
+#define CGS_RR3 (CGS_RECREG != 0)
+#endif
+#ifndef CGS_RRY
+#define CGS_RRY (CGS_RECREG >= 2)
+#endif
+#if CGS_RR0 && CGS_REC_SPLIT
+#error "CGS_RR0 keeps wave 0's own records: not with CGS_REC_SPLIT"
 #endif
 // CGS_E_RAWD: wave 2 loads the raw 2x2 block D (a, c, d planes) of stage E's
 // row itself (L2-resident: wave 0 read it 9 steps earlier) instead of
@@ -1510,7 +1526,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
         RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
         // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
-#if CGS_RECREG
+#if CGS_RR0
         const cg_f2 wu[2] = {QA[R2(-2)].wy[0], QA[R2(-2)].wy[1]};  // before row n takes the slot
         const CgRec q1 = QA[R2(-1)];
         QA[R2(0)] = put_rec(n, SG[RSG(0)]);
@@ -1541,7 +1557,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         const float4 a = s_y[t & 7][lane];
         return cg_f4{a.x, a.y, a.z, a.w};
       };
-#if CGS_RECREG
+#if CGS_RR1
       CgRec QB[4];  // records of rows n - 3 .. n - 6 (rows above the band: zero, as in LDS)
 #pragma unroll
       for (int m = 0; m < 4; ++m) QB[m] = CgRec{};
@@ -1553,17 +1569,17 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   cg_f2 w[2];         \
   get_wy(n + (d), w)
 #endif
-#if CGS_RECREG >= 2
+#if CGS_RRY
       cg_f4 Y1[8] = {zero4, zero4, zero4, zero4, zero4, zero4, zero4, zero4};  // y rows n-2 .. n-6
 #define CGS_Y1(d) Y1[R8(d)]
 #else
 #define CGS_Y1(d) yrow(n + (d))
 #endif
       CGS_STEPS({
-#if CGS_RECREG >= 2
+#if CGS_RRY
         Y1[R8(-2)] = yrow(n - 2);
 #endif
-#if CGS_RECREG
+#if CGS_RR1
         CGS_WY1(-7, w7);  // row n-7's vertical weights, before row n-3 takes its slot
         QB[R4(-3)] = get_rec(n - 3);
 #else
@@ -1599,14 +1615,14 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #undef CGS_Y1
     } else if (role == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
-#if CGS_RECREG
+#if CGS_RR2
       CgRec QC[2] = {CgRec{}, CgRec{}};  // records of rows n - 8, n - 9
 #endif
-#if CGS_RECREG >= 2
+#if CGS_RRY
       cg_f4 G1[4] = {zero4, zero4, zero4, zero4};  // g1 rows n-7 .. n-9
 #endif
       CGS_STEPS({
-#if CGS_RECREG
+#if CGS_RR2
         const cg_f2 w10[2] = {QC[R2(-10)].wy[0], QC[R2(-10)].wy[1]};  // before row n-8 takes the slot
         QC[R2(-8)] = get_rec(n - 8);
 #endif
@@ -1615,7 +1631,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         if (CGS_E_RAWD) load_acd(n + CGS_PF2 - 9, RD[RW2(CGS_PF2 - 9)]);
         // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
-#if CGS_RECREG
+#if CGS_RR2
           const CgRec q4 = QC[R2(-8)];
           const cg_f2 wu[2] = {QC[R2(-9)].wy[0], QC[R2(-9)].wy[1]};
 #else
@@ -1623,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 9, wu);
 #endif
-#if CGS_RECREG >= 2
+#if CGS_RRY
           G1[R4(-7)] = ld4(s_g1, n - 7);
           const cg_f4 ng = cgr_nsum_p(G1[R4(-9)], G1[R4(-8)], G1[R4(-7)], q4, wu);
 #else
@@ -1648,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         }
         // E) row n-9: q = A p, y_q = D^-1 q
         {
-#if CGS_RECREG
+#if CGS_RR2
           const CgRec q5 = QC[R2(-9)];
           const cg_f2(&wu)[2] = w10;
 #else
@@ -1675,14 +1691,14 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       // T5 = v2.N v2 (row n-12; T5 counts each edge once, by its right /
       // lower pixel)
       cg_f4 V1[4] = {zero4, zero4, zero4, zero4}, V2[2] = {zero4, zero4};
-#if CGS_RECREG
+#if CGS_RR3
       CgRec QD[2] = {CgRec{}, CgRec{}};  // records of rows n - 11, n - 12
 #endif
-#if CGS_RECREG >= 2
+#if CGS_RRY
       cg_f4 YQ[4] = {zero4, zero4, zero4, zero4};  // y_q rows n-10 .. n-12
 #endif
       CGS_STEPS({
-#if CGS_RECREG
+#if CGS_RR3
         const cg_f2 w13[2] = {QD[R2(-13)].wy[0], QD[R2(-13)].wy[1]};  // before row n-11 takes the slot
         QD[R2(-11)] = get_rec(n - 11);
 #endif
@@ -1690,7 +1706,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         // reads it at step n + 1
         if (CGS_REC_SPLIT) convert_rec(n);
         {
-#if CGS_RECREG
+#if CGS_RR3
           const CgRec q6 = QD[R2(-11)];
           const cg_f2 wu[2] = {QD[R2(-12)].wy[0], QD[R2(-12)].wy[1]};
 #else
@@ -1698,7 +1714,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           cg_f2 wu[2];
           get_wy(n - 12, wu);
 #endif
-#if CGS_RECREG >= 2
+#if CGS_RRY
           YQ[R4(-10)] = ld4(s_yq, n - 10);
           const cg_f4 yq = YQ[R4(-11)];
           const cg_f4 ny = cgr_nsum_p(YQ[R4(-12)], yq, YQ[R4(-10)], q6, wu);
@@ -1715,7 +1731,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           }
         }
         {
-#if CGS_RECREG
+#if CGS_RR3
           const CgRec q7 = QD[R2(-12)];
           const cg_f2(&wy7)[2] = w13;
 #else
