@@ -520,6 +520,12 @@ typedef float wmf_v2f __attribute__((ext_vector_type(2)));
 #ifndef WMF_SHIFT
 #define WMF_SHIFT 0
 #endif
+// WMF_XCD: blocks b, b + 8, b + 16 ... run on one XCD (one L2), so give each
+// XCD a contiguous run of row-major tiles; the 22x22 regions of horizontally
+// adjacent tiles (8 apart) then overlap inside one L2 instead of eight
+#ifndef WMF_XCD
+#define WMF_XCD 1
+#endif
 __device__ __forceinline__ float wmf_shl1(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x101, 0xf, 0xf, true));
 }
@@ -676,7 +682,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
   uint16_t *ku = reinterpret_cast<uint16_t *>(smp + RW * RP), *kv = ku + N;
   uint8_t *cid = reinterpret_cast<uint8_t *>(kv + N);
-  const int ty0 = blockIdx.y * WMF_T, tx0 = blockIdx.x * WMF_T;
+  int tbx = blockIdx.x, tby = blockIdx.y;
+  if (WMF_XCD) {
+    const int nt = gridDim.x * gridDim.y, lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const int xcd = lin & 7, tile = xcd * (nt >> 3) + min(xcd, nt & 7) + (lin >> 3);
+    tby = tile / gridDim.x;
+    tbx = tile - tby * gridDim.x;
+  }
+  const int ty0 = tby * WMF_T, tx0 = tbx * WMF_T;
   const int lane = threadIdx.x;
   WMF_STAMP(0);
   uint64_t a[NPER], b[NPER];

@@ -5,7 +5,7 @@
 set -u
 OUT=gpurun_out/r4_cgs_ab.log
 : > $OUT
-for rep in 1 2 3; do
+for rep in 1 2; do
 for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_cgs_rr23.so; do
   echo "== $L rep $rep" >> $OUT
   OPTFLOW_LIB=$L timeout -k 10 120 python -u tools/pcg_bench.py --iters 200 2>&1 | grep '"variant"' | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']['pcg_iter']; print('k_cgs 1080p us/launch', round(k['ms_per_launch']*1e3,2), 'rel_res', d['rel_res'])" >> $OUT || exit 1
