@@ -1,12 +1,12 @@
 #!/bin/bash
-# round 4: WMF XCD-aware tile order (in-tree, WMF_XCD=1) vs row-major
-# blockIdx tiles (lib_wmf_noxcd.so): isolated 1080p WMF launch time (bench lanes=1 replay),
+# round 4: WMF one list per wave (k_wmf2, lib_wmf_split.so) vs both lists per
+# wave (k_wmf, in-tree): isolated 1080p WMF launch time (bench lanes=1 replay),
 # the headline, and the flow's sha1 (must agree)
 set -u
 OUT=gpurun_out/r4_wmf_ab.log
 : > $OUT
 for rep in 1 2; do
-for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_wmf_noxcd.so; do
+for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_wmf_split.so; do
   echo "== $L rep $rep" >> $OUT
   if [ $rep = 1 ]; then
     OPTFLOW_LIB=$L timeout -k 10 120 python -u tools/ab/bitwise.py 540 960 >> $OUT 2>&1 || exit 1
