@@ -14,19 +14,6 @@
 #define OF_WAVE 64
 #define OF_BX 64  // block x = one wave across a row
 #define OF_BY 4   // 4 rows per block -> 256 threads
-// OF_PRIO_MODE (A/B knob): 1 = the warp / assembly / update kernels issue at
-// priority 1, 2 = the weighted median does (0: every kernel but k_cgs at 0)
-#ifndef OF_PRIO_MODE
-#define OF_PRIO_MODE 0
-#endif
-#define OF_PRIO_PATH()                                          \
-  do {                                                          \
-    if (OF_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(1);       \
-  } while (0)
-#define OF_PRIO_WMF()                                           \
-  do {                                                          \
-    if (OF_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(1);       \
-  } while (0)
 
 static inline int of_pitch(int W) { return (W + 63) & ~63; }
 

@@ -1172,17 +1172,13 @@ void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &
                      2 * (size_t)npow2 * sizeof(uint16_t) + 2 * (size_t)RW * RP;
   dim3 grid((uv.W + WMF_T - 1) / WMF_T, (uv.H + WMF_T - 1) / WMF_T);
   const float nk = (float)(-1.4426950408889634 / (2.0 * sigma_i * sigma_i));  // -log2(e) / (2 sigma^2)
-  const dim3 block(WMF_SPLIT ? 128 : 64);
+  const dim3 block(64);
   auto pick = [&](auto k1, auto k2, auto k4, auto k8, auto k8h7, auto k16) {
     auto k = nper == 1 ? k1 : nper == 2 ? k2 : nper == 4 ? k4 : nper == 8 ? (hsz == 7 ? k8h7 : k8) : k16;
     launch(c, "wmf", k, grid, block, shm, (const float2 *)uv.p, (const float *)guide.p, occ, out.p, uv.H, uv.W,
            uv.P, guide.ps(), hsz, nk, RW, RP, base);
   };
-  if (WMF_SPLIT && guide.C == 3)
-    pick(k_wmf2<3, 1, 0>, k_wmf2<3, 2, 0>, k_wmf2<3, 4, 0>, k_wmf2<3, 8, 0>, k_wmf2<3, 8, 7>, k_wmf2<3, 16, 0>);
-  else if (WMF_SPLIT)
-    pick(k_wmf2<1, 1, 0>, k_wmf2<1, 2, 0>, k_wmf2<1, 4, 0>, k_wmf2<1, 8, 0>, k_wmf2<1, 8, 7>, k_wmf2<1, 16, 0>);
-  else if (guide.C == 3)
+  if (guide.C == 3)
     pick(k_wmf<3, 1, 0>, k_wmf<3, 2, 0>, k_wmf<3, 4, 0>, k_wmf<3, 8, 0>, k_wmf<3, 8, 7>, k_wmf<3, 16, 0>);
   else
     pick(k_wmf<1, 1, 0>, k_wmf<1, 2, 0>, k_wmf<1, 4, 0>, k_wmf<1, 8, 0>, k_wmf<1, 8, 7>, k_wmf<1, 16, 0>);

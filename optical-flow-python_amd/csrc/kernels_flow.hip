@@ -133,7 +133,6 @@ template <int INTERP>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H,
                                                                 int W, int P, size_t ps, float *__restrict__ It,
                                                                 float *__restrict__ Ix, float *__restrict__ Iy) {
-  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -165,7 +164,6 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
                                 const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
                                 int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
-  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -307,7 +305,6 @@ __device__ __forceinline__ float2 upd(const float2 *uv, const float2 *x, size_t 
 __global__ void k_update_occ(const float2 *__restrict__ uv, const float2 *__restrict__ x, int clip,
                              float2 *__restrict__ uv1, const float *__restrict__ I1, const float *__restrict__ I2,
                              int nc, float *__restrict__ occ, int H, int W, int P, size_t ps) {
-  OF_PRIO_PATH();
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
@@ -509,41 +506,12 @@ struct WmfRec<1> {
 
 typedef float wmf_v2f __attribute__((ext_vector_type(2)));
 
-// WMF_SHIFT: in the window pass (compile-time window), lane px of a tile row
-// takes region column px + dx from lane px + 1's column of the previous step
-// (DPP row_shl:1) instead of reading it from LDS again; only the last lane of
-// each 8-lane tile row (px = 7, lanes 7 / 15 of a 16-lane DPP row) reads the
-// new column.  The same records in the same order: bitwise the same sums.
-// Measured (profiles/r4j_wmf_shift_ab.log): 0.918 vs 0.771 ms per 1080p
-// launch — the 5 DPP moves + select per sample cost more VALU than the LDS
-// reads they save; the pass is VALU / latency bound, not LDS bound.  Off.
-#ifndef WMF_SHIFT
-#define WMF_SHIFT 0
-#endif
 // WMF_XCD: blocks b, b + 8, b + 16 ... run on one XCD (one L2), so give each
 // XCD a contiguous run of row-major tiles; the 22x22 regions of horizontally
 // adjacent tiles (8 apart) then overlap inside one L2 instead of eight
 #ifndef WMF_XCD
 #define WMF_XCD 1
 #endif
-// WMF_SPLIT: k_wmf2 (one list per wave, two waves per tile) instead of k_wmf.
-// Measured (profiles/r4r_wmf_split_ab.log): 0.774 vs 0.768 ms per 1080p
-// launch, the same flow bitwise and 100 % exact on the WMF tests — twice the
-// waves per CU and half the sort per wave buy back exactly the weights both
-// waves now compute.  Off.
-#ifndef WMF_SPLIT
-#define WMF_SPLIT 0
-#endif
-__device__ __forceinline__ float wmf_shl1(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x101, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float4 wmf_shl1(const float4 &v) {
-  return make_float4(wmf_shl1(v.x), wmf_shl1(v.y), wmf_shl1(v.z), wmf_shl1(v.w));
-}
-__device__ __forceinline__ float2 wmf_shl1(const float2 &v) { return make_float2(wmf_shl1(v.x), wmf_shl1(v.y)); }
-__device__ __forceinline__ unsigned wmf_shl1(unsigned v) {
-  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, true);
-}
 
 // weight of region sample s for a pixel of guide colour (c01, c2):
 // max(2^(nk |dlab|^2) occ, 1e-10), channels 0-1 in packed fp32.  Called from
@@ -657,48 +625,6 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
   }
 }
 
-// bitonic_regs2 for one list (k_wmf2: one list per wave)
-template <int NPER>
-__device__ __forceinline__ void bitonic_regs1(uint64_t (&ka)[NPER], int lane) {
-  constexpr int N = NPER * 64;
-#pragma unroll
-  for (int kk = 2; kk <= N; kk <<= 1) {
-#pragma unroll
-    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-      if (jj >= NPER) {
-        const int lj = jj / NPER;
-        const bool take_min = ((lane & lj) == 0) == (((lane * NPER) & kk) == 0);
-        if (lj == 16 || lj == 32) {
-#pragma unroll
-          for (int r = 0; r < NPER; ++r) {
-            uint64_t p0, p1;
-            swap_lane64(ka[r], lj, p0, p1);
-            ka[r] = ((p0 < p1) == take_min) ? p0 : p1;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < NPER; ++r) {
-            const uint64_t oa = xor_lane64(ka[r], lj);
-            ka[r] = ((ka[r] < oa) == take_min) ? ka[r] : oa;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < NPER; ++r) {
-          const int rp = r ^ jj;
-          if (rp > r) {
-            const bool up = (((lane * NPER + r) & kk) == 0);
-            const uint64_t a0 = ka[r], a1 = ka[rp];
-            const bool sa = (a0 > a1) == up;
-            ka[r] = sa ? a1 : a0;
-            ka[rp] = sa ? a0 : a1;
-          }
-        }
-      }
-    }
-  }
-}
-
 // HS > 0: area_hsz fixed at compile time (window loop fully unrolled,
 // immediate LDS offsets); HS == 0: runtime hsz.  RP = LDS row pitch of the
 // region records (RP % 16 == 8: the 8 rows of a tile fall on disjoint banks).
@@ -710,7 +636,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
                                              int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt,
                                              const float2 *base) {
   using T = typename WmfRec<GC>::T;
-  OF_PRIO_WMF();
   constexpr int N = NPER * 64, CH = N / WMF_NC;
   const int hsz = HS > 0 ? HS : hsz_rt;
   // region width and record pitch: compile-time with HS (no runtime divides)
@@ -818,43 +743,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
       }
   };
-  // WMF_SHIFT form of visit_row (compile-time window only)
-  auto visit_row_shift = [&](int q0) {
-    constexpr int MX = 2 * HS + 1;
-    const bool edge = px == 7;
-    auto ids = [&](int q) {
-      if (WMF_CID_PAIR) return (unsigned)reinterpret_cast<const uint16_t *>(cid)[q];
-      return (unsigned)cid[q] | ((unsigned)cid[RW * RP + q] << 8);
-    };
-    T ext[MX > 1 ? MX : 2];
-    unsigned eid[MX > 1 ? MX : 2];
-#pragma unroll
-    for (int dx = 1; dx < MX; ++dx)
-      if (edge) {
-        ext[dx] = smp[q0 + dx];
-        eid[dx] = ids(q0 + dx);
-      }
-    T cur = smp[q0];
-    unsigned id = ids(q0);
-#pragma unroll
-    for (int dx = 0; dx < MX; ++dx) {
-      if (dx > 0) {
-        cur = wmf_shl1(cur);
-        id = wmf_shl1(id);
-        if (edge) {
-          cur = ext[dx];
-          id = eid[dx];
-        }
-      }
-      const wmf_sum_t w = (wmf_sum_t)wmf_w(cur, c01, cg[2], nk);
-      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + ((id & 0xffu) << WMF_SUM_SHIFT)), w);
-      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + ((id >> 8) << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
-    }
-  };
-  if (HS > 0 && WMF_SHIFT) {
-#pragma unroll
-    for (int dy = 0; dy <= 2 * HS; ++dy) visit_row_shift(qb + dy * RP);
-  } else if (HS > 0) {
+  if (HS > 0) {
 #pragma unroll
     for (int dy = 0; dy <= 2 * HS; ++dy) visit_row(qb + dy * RP, 2 * HS + 1);
   } else {
@@ -935,172 +824,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     out[(size_t)gi * P + gj] = med;
   }
 }
-// WMF_SPLIT form: a block of two waves per 8x8 tile, wave L (0: u, 1: v)
-// sorts and scans list L only, on the same LDS layout as k_wmf (records and
-// the list's chunk ids, chunk sums and sorted positions).  Each wave does half
-// the sort, one chunk-sum add per window sample and one walk, at twice the
-// waves per CU (the LDS of one k_wmf wave now serves two).  The same sums in
-// the same order per list (the v list's half-weight threshold is the u list's
-// total, read after a barrier, as in k_wmf): the same output.
-template <int GC, int NPER, int HS>
-__global__ __launch_bounds__(128) void k_wmf2(const float2 *__restrict__ uv, const float *__restrict__ guide,
-                                              const float *__restrict__ occ, float2 *out, int H, int W, int P,
-                                              size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt,
-                                              const float2 *base) {
-  using T = typename WmfRec<GC>::T;
-  constexpr int N = NPER * 64, CH = N / WMF_NC;
-  const int hsz = HS > 0 ? HS : hsz_rt;
-  constexpr int RWc = WMF_T + 2 * HS, RPc = RWc + ((8 - RWc) % 16 + 16) % 16;
-  const int RW = HS > 0 ? RWc : RW_rt, RP = HS > 0 ? RPc : RP_rt;
-  const bool fold1 = H >= WMF_T + hsz && W >= WMF_T + hsz;
-  auto mir = [&](int i, int n) { return fold1 ? (i < 0 ? -i : (i >= n ? 2 * (n - 1) - i : i)) : ext_mirror(i, n); };
-  const int nreg = RW * RW;
-  extern __shared__ double lds_f64[];
-  wmf_sum_t *csum = reinterpret_cast<wmf_sum_t *>(lds_f64);
-  T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
-  uint16_t *ku = reinterpret_cast<uint16_t *>(smp + RW * RP);
-  uint8_t *cid = reinterpret_cast<uint8_t *>(ku + 2 * N);
-  int tbx = blockIdx.x, tby = blockIdx.y;
-  if (WMF_XCD) {
-    const int nt = gridDim.x * gridDim.y, lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const int xcd = lin & 7, tile = xcd * (nt >> 3) + min(xcd, nt & 7) + (lin >> 3);
-    tby = tile / gridDim.x;
-    tbx = tile - tby * gridDim.x;
-  }
-  const int ty0 = tby * WMF_T, tx0 = tbx * WMF_T;
-  const int lane = threadIdx.x & 63;
-  const int L = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint16_t *kl = ku + L * N;
-  uint8_t *cl = cid + L * RW * RP;
-  uint64_t a[NPER];
-#pragma unroll
-  for (int r = 0; r < NPER; ++r) {
-    const int s = lane * NPER + r;
-    a[r] = ~0ull;
-    if (s < nreg) {
-      const int ry = s / RW, rx = s - ry * RW;
-      const size_t g = (size_t)mir(ty0 - hsz + ry, H) * P + mir(tx0 - hsz + rx, W);
-      const float2 v = uv[g];
-      a[r] = ((uint64_t)f2ord(L ? v.y : v.x) << 32) | ((uint64_t)ry << 8) | (uint64_t)rx;
-      if ((r & 1) == L || NPER == 1) {  // the two waves load half the records each
-        if (NPER > 1 || L == 0) {
-          float gv[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-          for (int c = 0; c < GC; ++c) gv[c] = guide[c * ps + g];
-          smp[ry * RP + rx] = WmfRec<GC>::make(gv[0], gv[1], gv[2], occ[g]);
-        }
-      }
-    }
-  }
-  wmf_sum_t *cs = csum + L * WMF_NC * 64 + lane;
-#pragma unroll
-  for (int c = 0; c < WMF_NC; ++c) cs[c * 64] = 0.0;
-  bitonic_regs1<NPER>(a, lane);
-#pragma unroll
-  for (int r = 0; r < NPER; ++r) {
-    const int e = lane * NPER + r;
-    const unsigned pa = (uint16_t)a[r];
-    kl[e] = (uint16_t)pa;  // padding keys -> 0xffff: out of every window
-    if (pa != 0xffffu) cl[(pa >> 8) * RP + (pa & 0xffu)] = (uint8_t)(e / CH);
-  }
-  __syncthreads();
-  const int py = lane >> 3, px = lane & 7;
-  const int gi = ty0 + py, gj = tx0 + px;
-  const int qb = py * RP + px;
-  float cg[3] = {0.f, 0.f, 0.f};
-  {
-    const T c0 = smp[qb + hsz * RP + hsz];
-    const float *cf = reinterpret_cast<const float *>(&c0);
-#pragma unroll
-    for (int c = 0; c < GC; ++c) cg[c] = cf[c];
-  }
-  const wmf_v2f c01 = {cg[0], cg[1]};
-  char *csb = reinterpret_cast<char *>(cs);
-  auto visit_row = [&](int q0, int n) {
-    constexpr int MX = HS > 0 ? 2 * HS + 1 : 5;
-    T rec[MX];
-    unsigned cu[MX];
-#pragma unroll
-    for (int dx = 0; dx < MX; ++dx)
-      if (dx < n) {
-        rec[dx] = smp[q0 + dx];
-        cu[dx] = cl[q0 + dx];
-      }
-#pragma unroll
-    for (int dx = 0; dx < MX; ++dx)
-      if (dx < n) {
-        const wmf_sum_t w = (wmf_sum_t)wmf_w(rec[dx], c01, cg[2], nk);
-        atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cu[dx] << WMF_SUM_SHIFT)), w);
-      }
-  };
-  if (HS > 0) {
-#pragma unroll
-    for (int dy = 0; dy <= 2 * HS; ++dy) visit_row(qb + dy * RP, 2 * HS + 1);
-  } else {
-    for (int dy = 0; dy <= 2 * hsz; ++dy)
-      for (int dx = 0; dx <= 2 * hsz; dx += 5) visit_row(qb + dy * RP + dx, min(5, 2 * hsz + 1 - dx));
-  }
-  __syncthreads();  // the u list's chunk sums: the total of both lists' thresholds
-  double sl[WMF_NC], tot = 0.0;
-#pragma unroll
-  for (int c = 0; c < WMF_NC; ++c) {
-    sl[c] = cs[c * 64];
-    tot += csum[c * 64 + lane];
-  }
-  const double half = 0.5 * tot;
-  double pl = 0.0, bl = 0.0, lbl = 0.0;
-  int ch = -1, last = 0;
-#pragma unroll
-  for (int c = 0; c < WMF_NC; ++c) {
-    if (ch < 0 && sl[c] > 0.0) { last = c; lbl = pl; }
-    if (ch < 0 && pl + sl[c] >= half) { ch = c; bl = pl; }
-    pl += sl[c];
-  }
-  if (ch < 0) { ch = last; bl = lbl; }
-  const unsigned span = 2u * hsz;
-  unsigned res = 0xffffu, lst = 0;
-  const uint4 *wl = reinterpret_cast<const uint4 *>(kl + ch * CH);
-  for (int g = 0; g < CH / 8; ++g) {
-    const uint4 A = wl[g];
-    const unsigned wa4[4] = {A.x, A.y, A.z, A.w};
-    unsigned ka[8];
-    bool ina[8];
-    T ra[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      ka[i] = (wa4[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu;
-      ina[i] = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
-      ra[i] = smp[ina[i] ? rya * RP + rxa : 0u];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float xa = wmf_w(ra[i], c01, cg[2], nk);
-      bl += ina[i] ? (double)xa : 0.0;
-      res = (res == 0xffffu && ina[i] && bl >= half) ? ka[i] : res;
-      lst = ina[i] ? ka[i] : lst;
-    }
-  }
-  if (res == 0xffffu) res = lst;
-  if (gi < H && gj < W) {
-    const int ya = mir(ty0 - hsz + (int)(res >> 8), H), xa = mir(tx0 - hsz + (int)(res & 0xffu), W);
-    const float2 sv = uv[(size_t)ya * P + xa];
-    float med = L ? sv.y : sv.x;
-    const size_t k = (size_t)gi * P + gj;
-    if (base) {
-      const float2 b0 = base[k];
-      const float bc = L ? b0.y : b0.x;
-      med = bc + (med - bc);
-    }
-    reinterpret_cast<float *>(out)[2 * k + L] = med;
-  }
-}
-#define OF_WMF2(GC, NP, HS)                                                                                       \
-  template __global__ void k_wmf2<GC, NP, HS>(const float2 *, const float *, const float *, float2 *, int, int, int, \
-                                               size_t, int, float, int, int, const float2 *);
-OF_WMF2(1, 1, 0) OF_WMF2(1, 2, 0) OF_WMF2(1, 4, 0) OF_WMF2(1, 8, 0) OF_WMF2(1, 16, 0) OF_WMF2(1, 8, 7)
-OF_WMF2(3, 1, 0) OF_WMF2(3, 2, 0) OF_WMF2(3, 4, 0) OF_WMF2(3, 8, 0) OF_WMF2(3, 16, 0) OF_WMF2(3, 8, 7)
-#undef OF_WMF2
 
 #define OF_WMF(GC, NP, HS)                                                                                       \
   template __global__ void k_wmf<GC, NP, HS>(const float2 *, const float *, const float *, float2 *, int, int, int, \
