@@ -1,12 +1,12 @@
 #!/bin/bash
-# round 4: WMF one list per wave (k_wmf2, lib_wmf_split.so) vs both lists per
-# wave (k_wmf, in-tree): isolated 1080p WMF launch time (bench lanes=1 replay),
-# the headline, and the flow's sha1 (must agree)
+# round 4: WMF two waves per tile with the window rows split (k_wmf3,
+# lib_wmf_halves.so) vs k_wmf (in-tree): isolated 1080p WMF launch time (bench lanes=1 replay),
+# the headline, and the flow's sha1 (k_wmf3 rounds the chunk sums differently)
 set -u
 OUT=gpurun_out/r4_wmf_ab.log
 : > $OUT
 for rep in 1 2; do
-for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_wmf_split.so; do
+for L in optical-flow-python_amd/optical_flow/_lib/liboptflow.so tools/ab/lib_wmf_halves.so; do
   echo "== $L rep $rep" >> $OUT
   if [ $rep = 1 ]; then
     OPTFLOW_LIB=$L timeout -k 10 120 python -u tools/ab/bitwise.py 540 960 >> $OUT 2>&1 || exit 1
