@@ -248,6 +248,10 @@ def wmf_compute_roofline(per_level):
         out.update({"valu_insts_per_launch": vi, "valu_insts_per_px": round(vi * 64 / px, 1),
                     "achieved": round(ach / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
                     "unit": "G wave-instr/s", "frac": round(ach / VALU_ISSUE_PEAK, 4)})
+    if rec.get("valu_pipe_busy") is not None:
+        # issue counts price every instruction at 2 cycles; the SQ's active
+        # cycles (fp64, transcendental, 64-bit ops take longer) give the pipe
+        out.update({"valu_pipe_busy": rec["valu_pipe_busy"], "valu_pipe_busy_source": rec.get("sq_source")})
     return out
 
 
