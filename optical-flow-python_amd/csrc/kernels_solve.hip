@@ -237,7 +237,6 @@ __device__ __forceinline__ CgInv cg_inv(const CgCoef &c) {
     float ic = 0.f;
     if (BLOCK) {
       // explicit fma: the same rounding wherever the inverse is formed
-      // (k_cgs forms it in two places, CGS_REC_SPLIT)
       const float det = __builtin_fmaf(a, d, -(cc * cc));
       const bool ok = det > 1e-30f * fabsf(a * d);
       const float inv = __builtin_amdgcn_rcpf(det);
@@ -559,72 +558,6 @@ __device__ __forceinline__ cg_f4 cgr_diag(const CgRec &m, cg_f4 f) {
     o[e] = da * fu + db * fv;
   }
   return cg_cat(o[0], o[1]);
-}
-// Pair-block splitting of k_cgs's preconditioner (CGS_PAIR): the lane's two
-// pixels (columns 2k, 2k+1 of the image, the same pairs in every tile) form
-// one 4x4 block D' = [[D0, -W], [-W, D1]] of A = D' - N', W = diag(wu, wv)
-// the weights of the edge inside the pair, N' = N without that edge.  The
-// Chebyshev polynomial is taken in B' = D'^-1 N' instead of D^-1 N, for the
-// same LDS record size: the record keeps D0^-1 in ma/mb[0] and S1^-1 =
-// (D1 - W D0^-1 W)^-1 (the Schur complement) in ma/mb[1].  Offline
-// (tools/pair_block_iters.py) it needed 0.75x the robust-stage iterations,
-// but those operators carry a row-only flow perturbation that makes the
-// horizontal edges dominate.  On the GPU (round 3, profiles/r3t_*): 479 ->
-// 449 CG iterations per 1080p pair, 48.8 -> 52.2 us per active 1080p launch
-// (the block elimination lengthens every stage's dependency chain), 38.29 vs
-// 38.42 pairs/s.  Off by default; kept as an A/B switch.
-#ifndef CGS_PAIR
-#define CGS_PAIR 0
-#endif
-// N' f (N f without the edge inside the pair)
-__device__ __forceinline__ cg_f4 cgr_nsum_p(cg_f4 up, cg_f4 mid, cg_f4 dn, const CgRec &c, const cg_f2 (&wu)[2]) {
-#if CGS_PAIR
-  const cg_f2 m0 = cg_lo(mid), m1 = cg_hi(mid);
-  const cg_f2 L = cg_left2(m1), Rt = cg_right2(m0), wl = cg_left2(c.wx[1]);
-  const cg_f2 s0 = wl * L + wu[0] * cg_lo(up) + c.wy[0] * cg_lo(dn);
-  const cg_f2 s1 = c.wx[1] * Rt + wu[1] * cg_hi(up) + c.wy[1] * cg_hi(dn);
-  return cg_cat(s0, s1);
-#else
-  return cgr_nsum(up, mid, dn, c, wu);
-#endif
-}
-// D'^-1 f by block elimination: y0' = D0^-1 f0, y1 = S1^-1 (f1 + W y0'),
-// y0 = y0' + D0^-1 W y1
-__device__ __forceinline__ cg_f4 cgr_pinv(const CgRec &m, cg_f4 r) {
-#if CGS_PAIR
-  const cg_f2 y0 = m.ma[0] * r.x + m.mb[0] * r.y;
-  const cg_f2 t = cg_hi(r) + m.wx[0] * y0;
-  const cg_f2 y1 = m.ma[1] * t.x + m.mb[1] * t.y;
-  const cg_f2 s = m.wx[0] * y1;
-  return cg_cat(y0 + (m.ma[0] * s.x + m.mb[0] * s.y), y1);
-#else
-  return cgr_minv(m, r);
-#endif
-}
-// D f (the 2x2 blocks of A) from a record: D0 re-formed from D0^-1, D1 =
-// S1 + W D0^-1 W with S1 re-formed from S1^-1
-__device__ __forceinline__ cg_f4 cgr_diag_p(const CgRec &m, cg_f4 f) {
-#if CGS_PAIR
-  cg_f2 o[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const float ia = m.ma[e].x, ic = m.ma[e].y, id = m.mb[e].y;
-    const float det = ia * id - ic * ic;
-    const float inv = det != 0.f ? __builtin_amdgcn_rcpf(det) : 0.f;
-    cg_f2 da = cg_f2{id, -ic} * inv, db = cg_f2{-ic, ia} * inv;
-    if (e == 1) {
-      const float wu = m.wx[0].x, wv = m.wx[0].y, ia0 = m.ma[0].x, ic0 = m.ma[0].y, id0 = m.mb[0].y;
-      const float cuv = wu * wv * ic0;
-      da += cg_f2{wu * wu * ia0, cuv};
-      db += cg_f2{cuv, wv * wv * id0};
-    }
-    const float fu = e ? f.z : f.x, fv = e ? f.w : f.y;
-    o[e] = da * fu + db * fv;
-  }
-  return cg_cat(o[0], o[1]);
-#else
-  return cgr_diag(m, f);
-#endif
 }
 // D f from the raw coefficient row (wave 0 still holds it): no inverse
 __device__ __forceinline__ cg_f4 cgr_diag_raw(const CgRaw &c, cg_f4 f) {
@@ -1156,93 +1089,25 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 // from one barrier per step: a stage reads rows of another wave produced at
 // earlier steps; the band is walked for n in [r0 - 8, r1 + 11] so that every
 // row a required stage reads was produced.
-// CGS_REC_SPLIT (default): wave 0 stores each coefficient row's record RAW
-// (edge weights final, the 2x2 block D as loaded) one row ahead, and wave 3
-// turns it into D^-1 in place one step later, so the inverse (a reciprocal
-// and ~12 multiplies per pixel pair) leaves wave 0, which set the pace of
-// the row step (round-3 phase timing: wave 0 102 K working cycles per
-// launch, wave 3 56 K).  The ring then holds one more row, and wave 0's
-// coefficient loads run one row further ahead (CGS_PF 3) so that a row's
-// load is still two steps from its first use.  Off (0): round 3's layout.
-// Measured (round 4, tools/ab/r4_cgs_ab.sh, 2 reps): 51.1 / 51.7 us per
-// isolated 1080p launch vs 48.9 / 49.2 without, headline 43.76 / 43.69 vs
-// 43.86 / 43.75 pairs/s, the same flow bitwise: wave 0's work does not set
-// the row step alone.  Off by default; kept as an A/B switch.
-#ifndef CGS_REC_SPLIT
-#define CGS_REC_SPLIT 0
-#endif
-#if CGS_REC_SPLIT && CGS_PAIR
-#error "CGS_REC_SPLIT does not form the CGS_PAIR Schur complement"
-#endif
-#define CGS_NREC (CGS_REC_SPLIT ? 15 : 14)
-// CGS_RECREG: each wave keeps the coefficient records of the rows it still
-// needs in a register ring and reads only one new record per row step from
-// the LDS ring (wave 0 none: it keeps the records it forms); CGS_RECREG >= 2
-// does the same for the stage rows y (wave 1), g1 (wave 2) and y_q (wave 3).
-// The stages read a record (64 B per lane) and the upper row's vertical
-// weights 9 + 9 times per step otherwise, ~45 KB of a block's ~65 KB of LDS
-// traffic per step.  Measured (profiles/r4e_cgs_recreg_ab.log): isolated
-// 1080p launch 50.1 vs 50.5 us (LDS bandwidth does not bound the step), the
-// timed bench 41.4 vs 44.2 pairs/s: 234 instead of 184 VGPRs leave a SIMD
-// that holds a k_cgs wave room for 2 instead of 3 of the other lanes' waves.
-// The flow also changes in the last bits (the compiler contracts the D^-1
-// products into the consumers once it sees them).  Off.
-#ifndef CGS_RECREG
-#define CGS_RECREG 0
-#endif
-// CGS_PRIO_ALL: waves 1 and 3 at issue priority 1 (0 otherwise), above the
+// Rejected variants of this kernel (record split over waves 0 / 3, register
+// record rings, raw-D stage E, pair-block splitting, trimmed drain loads)
+// are recorded with their measurements in DESIGN.md §3; the commits that
+// measured them hold their source.
+#define CGS_NREC 14
+// Waves 1 and 3 run at issue priority 1 (0 otherwise), above the
 // other lanes' kernels that share their SIMDs in the timed geometry: 45.65 /
 // 45.78 / 45.87 vs 45.34 / 45.45 / 45.57 pairs/s, 3 reps each
 // (profiles/r4k_prio_ab.log); the same arithmetic
 
-#ifndef CGS_PRIO_ALL
-#define CGS_PRIO_ALL 1
-#endif
-// per-wave form (A/B): CGS_RR<role> = 1 gives that wave its register ring
-#ifndef CGS_RR0
-#define CGS_RR0 (CGS_RECREG != 0)
-#endif
-#ifndef CGS_RR1
-#define CGS_RR1 (CGS_RECREG != 0)
-#endif
-#ifndef CGS_RR2
-#define CGS_RR2 (CGS_RECREG != 0)
-#endif
-#ifndef CGS_RR3
-#define CGS_RR3 (CGS_RECREG != 0)
-#endif
-#ifndef CGS_RRY
-#define CGS_RRY (CGS_RECREG >= 2)
-#endif
-#if CGS_RR0 && CGS_REC_SPLIT
-#error "CGS_RR0 keeps wave 0's own records: not with CGS_REC_SPLIT"
-#endif
-// CGS_E_RAWD: wave 2 loads the raw 2x2 block D (a, c, d planes) of stage E's
-// row itself (L2-resident: wave 0 read it 9 steps earlier) instead of
-// re-forming D from the record's D^-1 (two reciprocals, ~20 VALU per pixel
-// pair).  q = A p is then formed from the exact operator; the iterate differs
-// from the re-formed-D one in the last bits.
-#ifndef CGS_E_RAWD
-#define CGS_E_RAWD 0
-#endif
 // Load distance in row steps (each step ends at a block barrier, so a load
 // issued at step n is waited for at step n + distance): wave 0's coefficient,
 // p_old and r_in rows (CGS_PF), wave 2's p_old and x rows (CGS_PF2).  Ring
 // sizes are powers of two dividing the 8-step unroll.
 #ifndef CGS_PF
-#define CGS_PF (CGS_REC_SPLIT ? 3 : 2)
+#define CGS_PF 2
 #endif
 #ifndef CGS_PF2
 #define CGS_PF2 1
-#endif
-// no loads past the last row the band's outputs depend on (the drain steps
-// of the walk; ~7 % of a band's reads).  Bitwise the same; as OOB offsets
-// 38.29 vs 38.40 pairs/s (no gain: the row step is not load-bound), and a
-// first version that skipped the loads and stage A by branches ran at 26.3
-// (the branches forced every outstanding load to be waited for)
-// (profiles/r3u_ab.log, r3v_ab.log).  Off by default.
-#ifndef CGS_TRIM
-#define CGS_TRIM 0
 #endif
 #define CGS_POW2(n) ((n) <= 1 ? 1 : (n) <= 2 ? 2 : (n) <= 4 ? 4 : 8)
 #define CGS_SGN CGS_POW2(CGS_PF + 2)
@@ -1315,15 +1180,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   const int r0 = flip ? H - rb1 : rb0, r1 = flip ? H - rb0 : rb1;
   const float c0 = g.poly[0], c1 = g.poly[1], c2 = g.poly[2], c3 = g.poly[3], c4 = g.poly[4], c5 = g.poly[5];
   auto orow = [&](int t) { return (unsigned)(flip ? H - 1 - t : t); };
-  // rows past vlim feed no output of the band (stage A is needed up to row
-  // r1 + 7, p_old up to r1 + 8): their loads take the out-of-range offset,
-  // which reads 0 without touching memory (CGS_TRIM; branch-free, so the
-  // load pipelining is unchanged)
-  const int vlim = CGS_TRIM ? min(H, r1 + 9) : H;
-  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)vlim ? orow(t) * rowb4 : CG_ROW_OOB); };
-  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)vlim ? orow(t) * rowb8 : CG_ROW_OOB); };
+  auto o4 = [&](int t) { return off4 + ((unsigned)t < (unsigned)H ? orow(t) * rowb4 : CG_ROW_OOB); };
+  auto o8 = [&](int t) { return off8 + ((unsigned)t < (unsigned)H ? orow(t) * rowb8 : CG_ROW_OOB); };
   auto o4w = [&](int t) {
-    return flip ? off4 + ((unsigned)t < (unsigned)min(H - 1, vlim) ? (unsigned)(H - 2 - t) * rowb4 : CG_ROW_OOB) : o4(t);
+    return flip ? off4 + ((unsigned)t < (unsigned)(H - 1) ? (unsigned)(H - 2 - t) * rowb4 : CG_ROW_OOB) : o4(t);
   };
   auto load_raw = [&](int t, CgRaw &c) {
     const unsigned v = o4(t), vw = o4w(t);
@@ -1342,51 +1202,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     cc.a = c.a;
     cc.c = c.c;
     cc.d = c.d;
-#if CGS_PAIR
-    // pixel 1's entry becomes the Schur complement S1 = D1 - W D0^-1 W
-    {
-      CgCoef c0 = cc;
-      const CgInv m0 = cg_inv<true>(c0);
-      const float wu = c.wxu.x, wv = c.wxv.x;
-      cc.a.y = c.a.y - wu * wu * m0.ia.x;
-      cc.c.y = c.c.y - wu * wv * m0.ic.x;
-      cc.d.y = c.d.y - wv * wv * m0.id.x;
-    }
-#endif
     const CgInv mi = cg_inv<true>(cc);
     float4 *q = &ring[rslot(t)][0][lane];
     q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
     q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
-    q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
-    q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
-    CgRec r;  // the record as get_rec reads it back
-    r.wx[0] = cg_f2{c.wxu.x, c.wxv.x};
-    r.wy[0] = cg_f2{c.wyu.x, c.wyv.x};
-    r.wx[1] = cg_f2{c.wxu.y, c.wxv.y};
-    r.wy[1] = cg_f2{c.wyu.y, c.wyv.y};
-    r.ma[0] = cg_f2{mi.ia.x, mi.ic.x};
-    r.mb[0] = cg_f2{mi.ic.x, mi.id.x};
-    r.ma[1] = cg_f2{mi.ia.y, mi.ic.y};
-    r.mb[1] = cg_f2{mi.ic.y, mi.id.y};
-    return r;
-  };
-  // CGS_REC_SPLIT: the record with D still raw (a, c, c, d) in its D^-1 slots
-  auto put_raw = [&](int t, const CgRaw &c) {
-    float4 *q = &ring[rslot(t)][0][lane];
-    q[0] = make_float4(c.wxu.x, c.wxv.x, c.wyu.x, c.wyv.x);
-    q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
-    q[128] = make_float4(c.a.x, c.c.x, c.c.x, c.d.x);
-    q[192] = make_float4(c.a.y, c.c.y, c.c.y, c.d.y);
-  };
-  // ... and its conversion to D^-1 (the same cg_inv as put_rec)
-  auto convert_rec = [&](int t) {
-    float4 *q = &ring[rslot(t)][0][lane];
-    const float4 r0 = q[128], r1 = q[192];
-    CgCoef cc;
-    cc.a = cg_f2{r0.x, r1.x};
-    cc.c = cg_f2{r0.y, r1.y};
-    cc.d = cg_f2{r0.w, r1.w};
-    const CgInv mi = cg_inv<true>(cc);
     q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
     q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
   };
@@ -1446,13 +1265,6 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
   // rings indexed by (row - ns) mod ring size)
   CgRaw SG[CGS_SGN], SGp[2];
   cg_f4 PO[8], RI[CGS_RIN], PO2[CGS_W2N], XI[CGS_W2N];
-  CgRaw RD[CGS_E_RAWD ? CGS_W2N : 1];  // wave 2: raw a, c, d of stage E's rows
-  auto load_acd = [&](int t, CgRaw &c) {
-    const unsigned v = o4(t);
-    c.a = cg_mask1<ODD>(cg_ld2(rc, v, 4 * ps4), ok1);
-    c.c = cg_mask1<ODD>(cg_ld2(rc, v, 5 * ps4), ok1);
-    c.d = cg_mask1<ODD>(cg_ld2(rc, v, 6 * ps4), ok1);
-  };
   if (live && role == 0) {
     load_raw(ns - 2, SGp[0]);
     load_raw(ns - 1, SGp[1]);
@@ -1469,7 +1281,6 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     for (int m = -8; m < CGS_PF2 - 8; ++m) {
       PO2[(m + 16) & (CGS_W2N - 1)] = load_po(ns + m);
       XI[(m + 16) & (CGS_W2N - 1)] = load_x(ns + m);
-      if (CGS_E_RAWD) load_acd(ns + m - 1, RD[(m - 1 + 16) & (CGS_W2N - 1)]);
     }
   }
   float alpha = 0.f, beta = 0.f;
@@ -1479,12 +1290,10 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     for (int m = 0; m < CGS_W2N; ++m) XI[m] = zero4;
 
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  CgRec QA[2];  // CGS_RECREG: wave 0's records of rows n - 1, n - 2
   if (live) {
     if (role == 0) {
-      QA[0] = put_rec(ns - 2, SGp[0]);  // ring slots of rows ns - 2, ns - 1 at u = 0
-      QA[1] = put_rec(ns - 1, SGp[1]);
-      if (CGS_REC_SPLIT) put_raw(ns, SG[0]);  // wave 3 converts it at step ns
+      put_rec(ns - 2, SGp[0]);  // ring slots of rows ns - 2, ns - 1 at u = 0
+      put_rec(ns - 1, SGp[1]);
     }
     __syncthreads();
     CGS_T0
@@ -1493,11 +1302,9 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     // per 1080p launch (A/B, profiles/r2z_cgs_setprio_ab.log; wave 0
     // alone: 51.3)
     if (role == 0 || role == 2) __builtin_amdgcn_s_setprio(2);
-#if CGS_PRIO_ALL
     // the Horner and T waves above other kernels' waves on their SIMD (the
     // timed lanes run a fine solve one block per CU beside other lanes' work)
     else __builtin_amdgcn_s_setprio(1);
-#endif
     // each wave runs its own role's loop (registers of one role only), one
     // block barrier per row step in every role (same step count)
 #define CGS_STEPS(...)                                                    \
@@ -1526,20 +1333,13 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
         RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
         // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
-#if CGS_RR0
-        const cg_f2 wu[2] = {QA[R2(-2)].wy[0], QA[R2(-2)].wy[1]};  // before row n takes the slot
-        const CgRec q1 = QA[R2(-1)];
-        QA[R2(0)] = put_rec(n, SG[RSG(0)]);
-#else
-        if (CGS_REC_SPLIT) put_raw(n + 1, SG[RSG(1)]);
-        else put_rec(n, SG[RSG(0)]);
+        put_rec(n, SG[RSG(0)]);
         const CgRec q1 = get_rec(n - 1);
         cg_f2 wu[2];
         get_wy(n - 2, wu);
-#endif
         cg_f4 r = RI[RRI(-1)];
         if (!FIRST) r -= alpha * (cgr_diag_raw(SG[RSG(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
-        const cg_f4 y = cgr_pinv(q1, r);
+        const cg_f4 y = cgr_minv(q1, r);
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
         if (o >= r0 && o < r1) {
@@ -1557,57 +1357,36 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         const float4 a = s_y[t & 7][lane];
         return cg_f4{a.x, a.y, a.z, a.w};
       };
-#if CGS_RR1
-      CgRec QB[4];  // records of rows n - 3 .. n - 6 (rows above the band: zero, as in LDS)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) QB[m] = CgRec{};
-#define CGS_REC1(d) QB[R4(d)]
-#define CGS_WY1(d, w) const cg_f2 w[2] = {QB[R4(d)].wy[0], QB[R4(d)].wy[1]}
-#else
 #define CGS_REC1(d) get_rec(n + (d))
 #define CGS_WY1(d, w) \
   cg_f2 w[2];         \
   get_wy(n + (d), w)
-#endif
-#if CGS_RRY
-      cg_f4 Y1[8] = {zero4, zero4, zero4, zero4, zero4, zero4, zero4, zero4};  // y rows n-2 .. n-6
-#define CGS_Y1(d) Y1[R8(d)]
-#else
 #define CGS_Y1(d) yrow(n + (d))
-#endif
       CGS_STEPS({
-#if CGS_RRY
-        Y1[R8(-2)] = yrow(n - 2);
-#endif
-#if CGS_RR1
-        CGS_WY1(-7, w7);  // row n-7's vertical weights, before row n-3 takes its slot
-        QB[R4(-3)] = get_rec(n - 3);
-#else
         CGS_WY1(-7, w7);
-#endif
         {
           const CgRec q = CGS_REC1(-3);
           CGS_WY1(-4, wu);
           const cg_f4 y0 = CGS_Y1(-3);
-          const cg_f4 ny = cgr_nsum_p(CGS_Y1(-4), y0, CGS_Y1(-2), q, wu);
-          G4[R4(-3)] = c4 * y0 + c5 * cgr_pinv(q, ny);
+          const cg_f4 ny = cgr_nsum(CGS_Y1(-4), y0, CGS_Y1(-2), q, wu);
+          G4[R4(-3)] = c4 * y0 + c5 * cgr_minv(q, ny);
         }
         {
           const CgRec q = CGS_REC1(-4);
           CGS_WY1(-5, wu);
-          const cg_f4 ng = cgr_nsum_p(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
-          G3[R4(-4)] = c3 * CGS_Y1(-4) + cgr_pinv(q, ng);
+          const cg_f4 ng = cgr_nsum(G4[R4(-5)], G4[R4(-4)], G4[R4(-3)], q, wu);
+          G3[R4(-4)] = c3 * CGS_Y1(-4) + cgr_minv(q, ng);
         }
         {
           const CgRec q = CGS_REC1(-5);
           CGS_WY1(-6, wu);
-          const cg_f4 ng = cgr_nsum_p(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
-          G2[R4(-5)] = c2 * CGS_Y1(-5) + cgr_pinv(q, ng);
+          const cg_f4 ng = cgr_nsum(G3[R4(-6)], G3[R4(-5)], G3[R4(-4)], q, wu);
+          G2[R4(-5)] = c2 * CGS_Y1(-5) + cgr_minv(q, ng);
         }
         {
           const CgRec q = CGS_REC1(-6);
-          const cg_f4 ng = cgr_nsum_p(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, w7);
-          st4(s_g1, n - 6, c1 * CGS_Y1(-6) + cgr_pinv(q, ng));
+          const cg_f4 ng = cgr_nsum(G2[R4(-7)], G2[R4(-6)], G2[R4(-5)], q, w7);
+          st4(s_g1, n - 6, c1 * CGS_Y1(-6) + cgr_minv(q, ng));
         }
       })
 #undef CGS_REC1
@@ -1615,39 +1394,18 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
 #undef CGS_Y1
     } else if (role == 2) {
       cg_f4 PP[4] = {zero4, zero4, zero4, zero4}, ZZ[2] = {zero4, zero4};
-#if CGS_RR2
-      CgRec QC[2] = {CgRec{}, CgRec{}};  // records of rows n - 8, n - 9
-#endif
-#if CGS_RRY
-      cg_f4 G1[4] = {zero4, zero4, zero4, zero4};  // g1 rows n-7 .. n-9
-#endif
       CGS_STEPS({
-#if CGS_RR2
-        const cg_f2 w10[2] = {QC[R2(-10)].wy[0], QC[R2(-10)].wy[1]};  // before row n-8 takes the slot
-        QC[R2(-8)] = get_rec(n - 8);
-#endif
         PO2[RW2(CGS_PF2 - 8)] = load_po(n + CGS_PF2 - 8);
         XI[RW2(CGS_PF2 - 8)] = load_x(n + CGS_PF2 - 8);
-        if (CGS_E_RAWD) load_acd(n + CGS_PF2 - 9, RD[RW2(CGS_PF2 - 9)]);
         // D) row n-8: z = c0 y + D^-1 N g1, p = z + beta p_old, x += alpha p_old
         {
-#if CGS_RR2
-          const CgRec q4 = QC[R2(-8)];
-          const cg_f2 wu[2] = {QC[R2(-9)].wy[0], QC[R2(-9)].wy[1]};
-#else
           const CgRec q4 = get_rec(n - 8);
           cg_f2 wu[2];
           get_wy(n - 9, wu);
-#endif
-#if CGS_RRY
-          G1[R4(-7)] = ld4(s_g1, n - 7);
-          const cg_f4 ng = cgr_nsum_p(G1[R4(-9)], G1[R4(-8)], G1[R4(-7)], q4, wu);
-#else
-          const cg_f4 ng = cgr_nsum_p(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
-#endif
+          const cg_f4 ng = cgr_nsum(ld4(s_g1, n - 9), ld4(s_g1, n - 8), ld4(s_g1, n - 7), q4, wu);
           const float4 b = s_y[(n - 8) & 7][lane];
           const cg_f4 yr = {b.x, b.y, b.z, b.w};
-          const cg_f4 z = c0 * yr + cgr_pinv(q4, ng);
+          const cg_f4 z = c0 * yr + cgr_minv(q4, ng);
           cg_f4 p = FIRST ? z : z + beta * PO2[RW2(-8)];
           const int o = n - 8;
           const bool rv = (unsigned)o < (unsigned)H;
@@ -1664,18 +1422,13 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         }
         // E) row n-9: q = A p, y_q = D^-1 q
         {
-#if CGS_RR2
-          const CgRec q5 = QC[R2(-9)];
-          const cg_f2(&wu)[2] = w10;
-#else
           const CgRec q5 = get_rec(n - 9);
           cg_f2 wu[2];
           get_wy(n - 10, wu);
-#endif
           const cg_f4 pm = PP[R4(-9)];
-          const cg_f4 q = (CGS_E_RAWD ? cgr_diag_raw(RD[RW2(-9)], pm) : cgr_diag_p(q5, pm)) -
+          const cg_f4 q = cgr_diag(q5, pm) -
                           cgr_nsum(PP[R4(-10)], pm, PP[R4(-8)], q5, wu);
-          const cg_f4 yq = cgr_pinv(q5, q);
+          const cg_f4 yq = cgr_minv(q5, q);
           st4(s_yq, n - 9, yq);
           const int o = n - 9;
           if (o >= r0 && o < r1) {
@@ -1691,38 +1444,16 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
       // T5 = v2.N v2 (row n-12; T5 counts each edge once, by its right /
       // lower pixel)
       cg_f4 V1[4] = {zero4, zero4, zero4, zero4}, V2[2] = {zero4, zero4};
-#if CGS_RR3
-      CgRec QD[2] = {CgRec{}, CgRec{}};  // records of rows n - 11, n - 12
-#endif
-#if CGS_RRY
-      cg_f4 YQ[4] = {zero4, zero4, zero4, zero4};  // y_q rows n-10 .. n-12
-#endif
       CGS_STEPS({
-#if CGS_RR3
-        const cg_f2 w13[2] = {QD[R2(-13)].wy[0], QD[R2(-13)].wy[1]};  // before row n-11 takes the slot
-        QD[R2(-11)] = get_rec(n - 11);
-#endif
         // row n's record: raw since wave 0 stored it at step n - 1; stage A
         // reads it at step n + 1
-        if (CGS_REC_SPLIT) convert_rec(n);
         {
-#if CGS_RR3
-          const CgRec q6 = QD[R2(-11)];
-          const cg_f2 wu[2] = {QD[R2(-12)].wy[0], QD[R2(-12)].wy[1]};
-#else
           const CgRec q6 = get_rec(n - 11);
           cg_f2 wu[2];
           get_wy(n - 12, wu);
-#endif
-#if CGS_RRY
-          YQ[R4(-10)] = ld4(s_yq, n - 10);
-          const cg_f4 yq = YQ[R4(-11)];
-          const cg_f4 ny = cgr_nsum_p(YQ[R4(-12)], yq, YQ[R4(-10)], q6, wu);
-#else
           const cg_f4 yq = ld4(s_yq, n - 11);
-          const cg_f4 ny = cgr_nsum_p(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
-#endif
-          const cg_f4 v1 = cgr_pinv(q6, ny);
+          const cg_f4 ny = cgr_nsum(ld4(s_yq, n - 12), yq, ld4(s_yq, n - 10), q6, wu);
+          const cg_f4 v1 = cgr_minv(q6, ny);
           V1[R4(-11)] = v1;
           const int o = n - 11;
           if (o >= r0 && o < r1) {
@@ -1731,29 +1462,19 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           }
         }
         {
-#if CGS_RR3
-          const CgRec q7 = QD[R2(-12)];
-          const cg_f2(&wy7)[2] = w13;
-#else
           const CgRec q7 = get_rec(n - 12);
           cg_f2 wy7[2];
           get_wy(n - 13, wy7);
-#endif
           const cg_f4 v1 = V1[R4(-12)];
-          const cg_f4 nv = cgr_nsum_p(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
-          const cg_f4 v2 = cgr_pinv(q7, nv);
+          const cg_f4 nv = cgr_nsum(V1[R4(-13)], v1, V1[R4(-11)], q7, wy7);
+          const cg_f4 v2 = cgr_minv(q7, nv);
           const cg_f4 vu = V2[R2(-13)];
           V2[R2(-12)] = v2;
           const int o = n - 12;
           if (o >= r0 && o < r1) {
             const cg_f2 w0 = cg_lo(v2), w1 = cg_hi(v2);
             const cg_f2 h0 = cg_left2(q7.wx[1]) * cg_left2(w1) + wy7[0] * cg_lo(vu);
-#if CGS_PAIR
-            (void)w0;  // N' has no edge inside the pair
-            const cg_f2 h1 = wy7[1] * cg_hi(vu);
-#else
             const cg_f2 h1 = q7.wx[0] * w0 + wy7[1] * cg_hi(vu);
-#endif
             const cg_f4 t = (c3 * v1 + c4 * v2) * nv + (2.0f * c5) * v2 * cg_cat(h0, h1);
             acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
           }

@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-4 validation in two calls (each under gpurun's 1200 s):
-#   tools/r4_final.sh TAG tests  -> every -m gpu test + smoke
-#   tools/r4_final.sh TAG bench  -> default bench, configs 2 / 3, file pipeline
+# validation of a tree in two calls (each under gpurun's 1200 s):
+#   tools/final.sh TAG tests  -> every -m gpu test + smoke
+#   tools/final.sh TAG bench  -> default bench, configs 2 / 3, file pipeline
 set -u
-TAG=${1:-r4f}
+TAG=${1:-final}
 PART=${2:-tests}
 export PYTHONDONTWRITEBYTECODE=1
 mkdir -p gpurun_out

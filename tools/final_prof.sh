@@ -1,8 +1,8 @@
 #!/bin/bash
-# round-4 profiles of the default bench: rocprofv3 kernel traces (timed lanes
+# profiles of the default bench (final tree of a round): rocprofv3 kernel traces (timed lanes
 # and isolated), PMC passes, then the summaries committed under profiles/
 set -u
-TAG=${1:-r4p}
+TAG=${1:-final}
 export PYTHONDONTWRITEBYTECODE=1
 tools/profile.sh $TAG || exit $?
 D=gpurun_out/prof_$TAG
