@@ -173,6 +173,12 @@ int of_set_profiling(of_ctx *ctx, int enable);
  *                        sweep count bitwise. */
 #define OF_OPT_SOR_PIPELINE 1
 int of_set_option(of_ctx *ctx, int option, int value);
+/* read an option, or a read-only counter of the context and its batch lanes:
+ *   OF_OPT_SOR_FALLBACKS  pipelined SOR solves whose sweep hand-off timed out
+ *                         and were redone by the per-sweep kernel (the same
+ *                         result; a sign of an oversubscribed GPU) */
+#define OF_OPT_SOR_FALLBACKS 2
+int of_get_option(of_ctx *ctx, int option, int64_t *value);
 /* kernel timing accumulated since enable: per kernel name total ms, launch
  * count and pixels processed (sum over launches of the level's H*W; ROF
  * counts H*W*channels); any output pointer may be NULL */

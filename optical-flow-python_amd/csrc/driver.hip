@@ -206,6 +206,12 @@ struct of_ctx {
   double *d_partials = nullptr;
   unsigned *d_sor_sync = nullptr;
   char *d_sorp = nullptr;  // k_sor_pipe sync words, partials (lazily allocated)
+  // k_sor_pipe's ring of sweep buffers: one per context, grown to the largest
+  // level seen (every SOR solve ends in a stream synchronisation, so the
+  // ring is free again when the next solve starts)
+  float2 *d_sor_ring = nullptr;
+  size_t sor_ring_cap = 0;  // bytes
+  int sor_fallbacks = 0;    // pipelined solves rerun per sweep (hand-off timeout)
   int opt_sor_pipe = 1;    // of_set_option(OF_OPT_SOR_PIPELINE)
   // solve log (of_set_solve_log): fp64 true residual of every solve
   int slog = 0;
@@ -1020,7 +1026,15 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     q.b = b.p;
     q.x0 = x.p;
     q.bstride = (size_t)H * b.P;
-    q.ring = (float2 *)c->arena.alloc(sizeof(float2) * q.bstride * S);
+    const size_t ring_bytes = sizeof(float2) * q.bstride * S;
+    if (ring_bytes > c->sor_ring_cap) {
+      if (c->d_sor_ring) HIPCHK(hipFree(c->d_sor_ring));
+      c->d_sor_ring = nullptr;
+      c->sor_ring_cap = 0;
+      HIPCHK(hipMalloc(&c->d_sor_ring, ring_bytes));
+      c->sor_ring_cap = ring_bytes;
+    }
+    q.ring = c->d_sor_ring;
     q.H = H;
     q.W = W;
     q.P = b.P;
@@ -1051,11 +1065,17 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
     HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_norm, q.fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    REQUIRE(*(const int *)c->h_norm == 0, OF_EHIP, "SOR sweep hand-off timed out");
-    const PcgState &st = c->h_state[0];
-    REQUIRE(st.done != 0, OF_EHIP, "SOR pipeline ended without a decided sweep");
-    note_active(c, "sor_pipe", st.iter, (double)H * W);
-    return {st.iter, st.done, st.xnorm2 > 0 ? std::sqrt(st.rr / st.xnorm2) : 0.0};
+    if (*(const int *)c->h_norm == 0) {
+      const PcgState &st = c->h_state[0];
+      REQUIRE(st.done != 0, OF_EHIP, "SOR pipeline ended without a decided sweep");
+      note_active(c, "sor_pipe", st.iter, (double)H * W);
+      return {st.iter, st.done, st.xnorm2 > 0 ? std::sqrt(st.rr / st.xnorm2) : 0.0};
+    }
+    // a hand-off wait timed out (e.g. the grid could not stay resident beside
+    // other lanes' work): k_sor_pipe_final left x = 0 and the state as
+    // k_sor_init set it, so the per-sweep kernel below redoes the solve from
+    // the start (the same iterate and sweep count bitwise)
+    ++c->sor_fallbacks;
   }
   double *sor_part = c->d_partials + 10 * PCG_MAX_BLOCKS;  // 2 x [2 * nstrips][2]
   auto args_k = [&](int k) {
@@ -1899,6 +1919,7 @@ int of_ctx_destroy(of_ctx *c) {
   hipFree(c->d_partials);
   hipFree(c->d_sor_sync);
   if (c->d_sorp) hipFree(c->d_sorp);
+  if (c->d_sor_ring) hipFree(c->d_sor_ring);
   hipFree(c->d_rpart);
   hipFree(c->d_rlog);
   hipFree(c->d_mm);
@@ -1928,6 +1949,24 @@ int of_set_option(of_ctx *c, int option, int value) {
     case OF_OPT_SOR_PIPELINE:
       c->opt_sor_pipe = value ? 1 : 0;
       return OF_OK;
+    default:
+      c->err = "unknown option";
+      return OF_EINVAL;
+  }
+}
+
+int of_get_option(of_ctx *c, int option, int64_t *value) {
+  if (!c || !value) return OF_EINVAL;
+  switch (option) {
+    case OF_OPT_SOR_PIPELINE:
+      *value = c->opt_sor_pipe;
+      return OF_OK;
+    case OF_OPT_SOR_FALLBACKS: {
+      int64_t n = c->sor_fallbacks;
+      for (of_ctx *l : c->lanes) n += l->sor_fallbacks;
+      *value = n;
+      return OF_OK;
+    }
     default:
       c->err = "unknown option";
       return OF_EINVAL;
@@ -2783,10 +2822,14 @@ int of_rccl_gather_flows(of_ctx *c, int nslots, float *out_uv_rank0) {
   const size_t per = 2 * (size_t)H * W;
   float *recv = nullptr;
   if (c->rank == 0) recv = (float *)c->arena.alloc(sizeof(float) * per * nslots * c->nranks);
+  // rank 0's own slots first: nothing that can throw runs between
+  // ncclGroupStart and ncclGroupEnd, so a failed copy cannot leave a group open
+  if (c->rank == 0)
+    for (int s = 0; s < nslots; ++s)
+      HIPCHK(hipMemcpyAsync(recv + per * s, c->slots[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
   ncclResult_t r = ncclGroupStart();
   for (int s = 0; s < nslots && r == ncclSuccess; ++s) {
     if (c->rank == 0) {
-      HIPCHK(hipMemcpyAsync(recv + per * s, c->slots[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
       for (int src = 1; src < c->nranks && r == ncclSuccess; ++src)
         r = ncclRecv(recv + per * ((size_t)src * nslots + s), per, ncclFloat, src, c->comm, c->stream);
     } else {

@@ -20,6 +20,7 @@ PENALTY = {
 }
 MAX_LEVELS = 32
 OF_OPT_SOR_PIPELINE = 1  # of_set_option
+OF_OPT_SOR_FALLBACKS = 2  # of_get_option (read-only counter)
 
 
 class OfPenalty(C.Structure):

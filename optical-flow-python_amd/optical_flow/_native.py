@@ -34,6 +34,7 @@ _SIGS = {
     "of_synchronize": ([_vp], C.c_int),
     "of_set_profiling": ([_vp, C.c_int], C.c_int),
     "of_set_option": ([_vp, C.c_int, C.c_int], C.c_int),
+    "of_get_option": ([_vp, C.c_int, C.POINTER(C.c_int64)], C.c_int),
     "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _dp, _ip], C.c_int),
     "of_kernel_timeline": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, _dp, _dp, _ip], C.c_int),
     "of_estimate_flow": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, C.c_int, _fp, _fp,
@@ -137,6 +138,12 @@ class Context:
     def set_option(self, option, value):
         """of_set_option (include/optflow.h), e.g. OF_OPT_SOR_PIPELINE."""
         self.check(self.lib.of_set_option(self.handle, int(option), int(value)))
+
+    def get_option(self, option):
+        """of_get_option: an option's value or a read-only counter (OF_OPT_SOR_FALLBACKS)."""
+        v = C.c_int64(0)
+        self.check(self.lib.of_get_option(self.handle, int(option), C.byref(v)))
+        return v.value
 
     def set_solve_log(self, enable=True):
         """Log the fp64 true residual of every linear solve (of_set_solve_log)."""

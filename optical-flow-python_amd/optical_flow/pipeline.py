@@ -83,13 +83,14 @@ def decode_pair(job):
     return _pair_of(job, load_frame(job.im1), load_frame(job.im2), read_flo(job.gt) if job.gt else None)
 
 
-def _finish(job, uv, gt, border, keep=False):
+def _finish(job, uv, gt, border, keep=False, planar=False):
     """Write the .flo and evaluate one pair (writer thread).  `uv` (H, W, 2),
-    or the library's (2, H, W) float32 planes (PairStream.wait(planar=True)):
-    then the .flo is written from the planes and the metrics take them as
-    they are (flow_angular_error computes in float64 either way, so the
-    numbers are the same), and only `keep` builds the (H, W, 2) float64 flow."""
-    planar = uv.ndim == 3 and uv.shape[0] == 2 and uv.dtype == np.float32
+    or with `planar` the library's (2, H, W) float32 planes
+    (PairStream.wait(planar=True)): then the .flo is written from the planes
+    and the metrics take them as they are (flow_angular_error computes in
+    float64 either way, so the numbers are the same), and only `keep` builds
+    the (H, W, 2) float64 flow.  The caller says which layout it passes (a
+    (2, W, 2) flow is both shapes)."""
     u, v = (uv[0], uv[1]) if planar else (uv[..., 0], uv[..., 1])
     res = {"name": job.name, "shape": u.shape, "out": job.out}
     if job.out:
@@ -191,8 +192,12 @@ def run_pipeline(jobs, method="classic+nl-fast", params=None, lanes=4, chunk=8, 
 # Open PairStreams kept between run_pipeline calls (a server's pool: lane
 # threads, contexts and arenas stay warm), keyed by (frame shape, method,
 # params, lanes); at most _MAX_STREAMS, the least recently used closed first.
+# One by default: a stream's lanes hold GPU_MAX_HW_QUEUES-sized stream sets
+# and their own fine-solve token, so two open pools would oversubscribe the
+# hardware queues and run their fine solves uncoordinated; a shape change
+# drains and closes the open pool.
 _STREAMS = OrderedDict()
-_MAX_STREAMS = 2
+_MAX_STREAMS = 1
 _STREAMS_LOCK = threading.Lock()
 
 
@@ -254,7 +259,7 @@ def _run_streaming(jobs, method, params, lanes, ahead_chunks, workers, writers, 
         def retire(key):
             i, t, gt = inflight[key].pop(0)
             uv = timed("gpu_s", streams[key].wait, t, True)  # planar: converted by the writer
-            writes.append((i, wr.submit(timed, "write_s", _finish, jobs[i], uv, gt, border, keep_flows)))
+            writes.append((i, wr.submit(timed, "write_s", _finish, jobs[i], uv, gt, border, keep_flows, True)))
 
         def drain(key):
             while inflight.get(key):

@@ -79,6 +79,29 @@ def test_pipeline_errors(tmp_path):
         run_pipeline(jobs, chunk=0, flow_fn=lambda a, b: [])
 
 
+def test_finish_layout_is_explicit(tmp_path):
+    """_finish takes the layout from its caller: a (2, W, 2) float32 flow in
+    (H, W, 2) layout (H == 2) is written and evaluated as such, not read as
+    planes."""
+    from optical_flow import flow_angular_error, read_flo
+    from optical_flow.pipeline import PairJob, _finish
+    rng = np.random.default_rng(3)
+    uv = rng.standard_normal((2, 7, 2)).astype(np.float32)
+    gt = rng.standard_normal((2, 7, 2)).astype(np.float32)
+    out = str(tmp_path / "a.flo")
+    r = _finish(PairJob("a", None, None, out=out), uv, gt, 0, keep=True)
+    np.testing.assert_array_equal(read_flo(out), uv)
+    assert r["shape"] == (2, 7)
+    want = flow_angular_error(gt[..., 0], gt[..., 1], uv[..., 0], uv[..., 1], 0)
+    np.testing.assert_allclose((r["aae"], r["std_ae"], r["aepe"]), want, rtol=1e-12)
+    # the same flow as planes, said so
+    out2 = str(tmp_path / "b.flo")
+    r2 = _finish(PairJob("b", None, None, out=out2), np.ascontiguousarray(np.moveaxis(uv, 2, 0)), gt, 0,
+                 keep=True, planar=True)
+    np.testing.assert_array_equal(read_flo(out2), uv)
+    np.testing.assert_allclose((r2["aae"], r2["std_ae"], r2["aepe"]), want, rtol=1e-12)
+
+
 def test_middlebury_jobs_layout(tmp_path):
     from optical_flow.pipeline import middlebury_jobs
     root = tmp_path / "data"
@@ -115,8 +138,8 @@ def test_pipeline_gpu_matches_estimate_flow(tmp_path, stream):
     syn = tmp_path / "syn"
     syn.mkdir()
     jobs += _write_pairs(syn, [(40, 56, 3), (48, 64, 1), (40, 56, 3), (40, 56, 3)], seed=5)
-    # three frame shapes: the streaming form keeps at most two PairStreams
-    # open and closes the least recently used one
+    # three frame shapes: the streaming form keeps one PairStream open (the
+    # default _MAX_STREAMS) and drains and closes it when the shape changes
     res, st = run_pipeline(jobs, lanes=3, chunk=2, keep_flows=True, stream=stream)
     print(f"pipeline: {st}")
     for j, r in zip(jobs, res):
@@ -131,10 +154,10 @@ def test_pipeline_gpu_matches_estimate_flow(tmp_path, stream):
     print(f"RubberWhale AAE {rw['aae']:.5f} AEPE {rw['aepe']:.6f} (reference 2.46298 / 0.080250)")
     assert abs(rw["aepe"] - 0.080250) <= 1e-3 and abs(rw["aae"] - 2.46298) <= 0.02
     if stream:
-        # the streams stay open for the next call (at most two), which gives
-        # the same flows; close_streams releases them
+        # the last stream stays open for the next call, which gives the same
+        # flows; close_streams releases it
         from optical_flow import pipeline as pl
-        assert 1 <= len(pl._STREAMS) <= 2
+        assert len(pl._STREAMS) == pl._MAX_STREAMS == 1
         res2, _ = run_pipeline(jobs, lanes=3, chunk=2, keep_flows=True)
         for r, q in zip(res, res2):
             np.testing.assert_array_equal(r["uv"], q["uv"])
