@@ -650,14 +650,20 @@ static int sor(const double *coef, const double *b, int H, int W, double omega, 
 }
 
 /* _solve_linear_system (base.py:87-114).  'backslash' (SuperLU) is restated as
- * a PCG solve to rtol 1e-12 (fp64), i.e. the direct solution to ~1e-10. */
+ * a PCG solve to rtol 1e-12 (fp64), i.e. the direct solution to ~1e-10.
+ * ofr_set_backslash_rtol (test-only experiment knob, tools/rtol_chaos.py):
+ * another stopping tolerance for that PCG, to separate the GPU surrogate's
+ * rtol from fp32 arithmetic; <= 0 restores 1e-12. */
+static double g_backslash_rtol = 1e-12;
+void ofr_set_backslash_rtol(double rtol) { g_backslash_rtol = rtol > 0 ? rtol : 1e-12; }
+
 int ofr_solve(const of_params *P, const double *coef, const double *rhs, int H, int W, double *x, int *iters,
               double *relres) {
   double rr = 0;
   int it;
   if (P->solver == OF_SOLVER_PCG) it = pcg(coef, rhs, H, W, P->pcg_rtol, P->pcg_maxiter, 0, x, &rr);
   else if (P->solver == OF_SOLVER_SOR) it = sor(coef, rhs, H, W, 1.9, P->sor_max_iters, 1e-2, x);
-  else it = pcg(coef, rhs, H, W, 1e-12, 100000, 1, x, &rr);
+  else it = pcg(coef, rhs, H, W, g_backslash_rtol, 100000, 1, x, &rr);
   if (iters) *iters = it;
   if (relres) *relres = rr;
   return 0;

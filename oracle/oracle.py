@@ -43,6 +43,7 @@ def lib():
                                               C.c_int, _dp, _dp]
         _lib.ofr_solve.argtypes = [C.POINTER(_abi.OfParams), _dp, _dp, C.c_int, C.c_int, _dp, _ip, _dp]
         _lib.ofr_num_threads.restype = C.c_int
+        _lib.ofr_set_backslash_rtol.argtypes = [C.c_double]
     return _lib
 
 
@@ -63,6 +64,12 @@ def unplanar(a, squeeze=True):
     if squeeze and a.shape[0] == 1:
         return a[0]
     return np.moveaxis(a, 0, 2).copy()
+
+
+def set_backslash_rtol(rtol):
+    """Test-only: stop the oracle's 'backslash' PCG at `rtol` instead of 1e-12
+    (None or <= 0 restores 1e-12).  Process-global."""
+    lib().ofr_set_backslash_rtol(C.c_double(float(rtol or 0.0)))
 
 
 def num_threads():
