@@ -7,15 +7,21 @@
 One process per GPU.  A step = every rank runs estimate_flow on its P
 pairs (default 8 = config 5's 64 pairs over 8 GPUs) with the frames already
 resident in HBM (uploaded to device slots before the timed region) and the
-flows left there (of_pairs_run: RGB -> gray/Lab, ROF, pyramids, GNC x levels
-x IRLS, L pairs in flight on concurrent streams); for N > 1 the flows are
-also gathered to rank 0 with RCCL over xGMI.  Timed region: barrier + device
-sync on both sides, max over ranks.  value = pairs processed by all ranks /
-time (weak scaling: P pairs per GPU).  Reported beside it: `host_to_host`
-(SURVEY.md §8d's form: uint8 frames in host memory -> H2D -> ... -> D2H of
-the fp32 flow, of_pairs_run_host, copies overlapped with compute; the
-PCIe-inclusive rate, never `value`) and `streamed` (the same host-to-host
-steps through the persistent pair pool, of_pairs_submit / of_pairs_wait).
+flows left there (RGB -> gray/Lab, ROF, pyramids, GNC x levels x IRLS, L
+pairs in flight on concurrent streams), through the persistent pair pool
+(of_pairs_open + of_pairs_submit_slots: step s+1 is queued before step s is
+waited for, so the lanes do not drain between steps; the steps alternate
+between two sets of P slots); for N > 1 each step's flows are also gathered
+to rank 0 with RCCL over xGMI (of_rccl_gather_slots).  Timed region: barrier
++ device sync on both sides, max over ranks.  value = pairs processed by all
+ranks / time (weak scaling: P pairs per GPU).  Reported beside it:
+`device_resident_drained` (the same steps as one of_pairs_run call each:
+the lanes drain at every step end), `host_to_host` (SURVEY.md §8d's form:
+uint8 frames in host memory -> H2D -> ... -> D2H of the fp32 flow,
+of_pairs_run_host, copies overlapped with compute; the PCIe-inclusive rate,
+never `value` -- the task's measurement contract puts the inputs in HBM)
+and `streamed` (host-to-host through the pool, of_pairs_submit /
+of_pairs_wait); all over the same K steps.
 
 Also reported (one JSON line on rank 0):
   roofline      dominant HBM kernel: algorithmic bytes per launch / mean
@@ -452,32 +458,69 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         ctx.check(lib.of_rccl_init(ctx.handle, obj[0], world, rank))
 
-    # the timed steps: frames resident in HBM (device slots, uploaded here,
-    # outside the timed region), flows left in HBM (+ the RCCL gather)
-    def upload_all():
-        for s, (a, b) in enumerate(zip(f1, f2)):
-            ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(_native.f32(a)), _native.ptr(_native.f32(b)),
-                                         H, W, 3))
+    # the timed steps: frames resident in HBM (two sets of device slots,
+    # uploaded here, outside the timed region), flows left in HBM (+ the RCCL
+    # gather), queued through the pair pool back to back
+    NP = args.pairs
+    sets = [(C.c_int * NP)(*range(k * NP, (k + 1) * NP)) for k in range(2)]
+
+    def upload_all(nsets=2):
+        for k in range(nsets):
+            for s, (a, b) in enumerate(zip(f1, f2)):
+                ctx.check(lib.of_pair_upload(ctx.handle, k * NP + s, _native.ptr(_native.f32(a)),
+                                             _native.ptr(_native.f32(b)), H, W, 3))
     upload_all()
+    ctx.check(lib.of_pairs_open(ctx.handle, H, W, 3, C.byref(P0), args.lanes))
 
-    def step():
-        run_step(ctx, P0, args.pairs, args.lanes)
+    def psubmit(s):
+        t = C.c_int64(0)
+        ctx.check(lib.of_pairs_submit_slots(ctx.handle, NP, sets[s % 2], C.byref(t)))
+        return t.value
+
+    def pwait(s, t0_):
+        for t in range(t0_, t0_ + NP):
+            ctx.check(lib.of_pairs_wait(ctx.handle, t))
         if world > 1:
-            ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
+            ctx.check(lib.of_rccl_gather_slots(ctx.handle, (s % 2) * NP, NP, None))
 
-    for _ in range(args.warmup):
-        step()
+    def pool_steps(k):
+        prev = psubmit(0)
+        for s in range(1, k):
+            cur = psubmit(s)
+            pwait(s - 1, prev)
+            prev = cur
+        pwait(k - 1, prev)
+
+    if args.warmup:
+        pool_steps(args.warmup)
     barrier(dist)
     ctx.check(lib.of_synchronize(ctx.handle))
     t0 = time.perf_counter()
+    pool_steps(args.steps)
+    ctx.check(lib.of_synchronize(ctx.handle))
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    value = world * NP * args.steps / elapsed
+    ctx.check(lib.of_pairs_close(ctx.handle))
+    dev_uv = np.empty((2, H, W), dtype=np.float32)  # the timed flow of pair 0 (last step's slot set)
+    ctx.check(lib.of_pair_download(ctx.handle, ((args.steps - 1) % 2) * NP, _native.ptr(dev_uv)))
+
+    # the same steps as one of_pairs_run call each (lanes drain at step end)
+    def step():
+        run_step(ctx, P0, NP, args.lanes)
+        if world > 1:
+            ctx.check(lib.of_rccl_gather_flows(ctx.handle, NP, None))
+    step()
+    barrier(dist)
+    ctx.check(lib.of_synchronize(ctx.handle))
+    td = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.check(lib.of_synchronize(ctx.handle))
     barrier(dist)
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
-    value = world * args.pairs * args.steps / elapsed
-    dev_uv = np.empty((2, H, W), dtype=np.float32)  # the timed flow of pair 0
-    ctx.check(lib.of_pair_download(ctx.handle, 0, _native.ptr(dev_uv)))
+    d_elapsed = max_over_ranks(dist, time.perf_counter() - td)
+    drained_uv = np.empty((2, H, W), dtype=np.float32)
+    ctx.check(lib.of_pair_download(ctx.handle, 0, _native.ptr(drained_uv)))
 
     # host to host (PCIe-inclusive): uint8 frames in host memory -> flows in
     # host memory, copies overlapped inside the library
@@ -485,7 +528,7 @@ def main():
         ctx.check(lib.of_pairs_run_host(ctx.handle, args.pairs, p1, p2, H, W, 3, C.byref(P0), args.lanes, po, None))
         if world > 1:
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
-    hsteps = max(1, min(args.steps, 3))
+    hsteps = args.steps
     hstep()  # warm-up (pinned staging buffers)
     barrier(dist)
     ctx.check(lib.of_synchronize(ctx.handle))
@@ -539,7 +582,7 @@ def main():
 
     # the host steps reused the device slots: upload the frames again for
     # the per-level pair and the profiled replays
-    upload_all()
+    upload_all(1)
     # per-level times + accuracy from one more (untimed) pair
     st = _abi.OfStats()
     P = _abi.OfParams()
@@ -606,7 +649,14 @@ def main():
                        "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
                        "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
             "timed_region": "frames resident in HBM (device slots, uploaded before the timed region) -> "
-                            "flows (fp32) left in HBM",
+                            "flows (fp32) left in HBM; K steps queued back to back through the pair pool "
+                            "(of_pairs_submit_slots)",
+            "device_resident_drained": {"value": round(world * NP * args.steps / d_elapsed, 4),
+                                        "ms_per_step": round(1e3 * d_elapsed / args.steps, 3),
+                                        "steps": args.steps,
+                                        "flow_equals_timed_flow": bool(np.array_equal(drained_uv, dev_uv)),
+                                        "note": "one of_pairs_run per step: the lanes drain at every step end "
+                                                "(rounds 1-4's device-resident form)"},
             "host_to_host": {"value": round(world * args.pairs * hsteps / h_elapsed, 4),
                              "ms_per_step": round(1e3 * h_elapsed / hsteps, 3), "steps": hsteps,
                              "host_flow_equals_timed_flow": host_eq_dev,

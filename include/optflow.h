@@ -179,6 +179,33 @@ int of_set_option(of_ctx *ctx, int option, int value);
  *                         result; a sign of an oversubscribed GPU) */
 #define OF_OPT_SOR_FALLBACKS 2
 int of_get_option(of_ctx *ctx, int option, int64_t *value);
+/* progress of compute_flow / compute_flow_base: the reference's `display`
+ * prints and its per-GNC-stage report (classic_nl.py:141-196, 255-256;
+ * ba.py:101-133, 189-190; hs.py:80-81, 123-124; alt_ba.py:128-183, 249-250).
+ * The callback runs on the calling thread, synchronously, between kernel
+ * launches.  Events: a GNC stage starts; a pyramid level starts; a warping /
+ * linear iteration's solve is done (with OF_PROGRESS_ITER: `norm` = the
+ * reference's ||x - duv|| after the clip, or HS's ||x||, in fp64 on the
+ * device -- one stream synchronisation per iteration); a GNC stage ends
+ * (`elapsed_s` after a stream synchronisation; with OF_PROGRESS_FLOW `uv`
+ * holds the stage's flow, planar 2 x h x w, valid during the call).  Batch
+ * entries (of_pairs_*) never report.  fn = NULL turns it off. */
+enum of_event { OF_EV_STAGE = 0, OF_EV_LEVEL = 1, OF_EV_ITER = 2, OF_EV_STAGE_END = 3 };
+#define OF_PROGRESS_ITER 1
+#define OF_PROGRESS_FLOW 2
+typedef struct of_progress {
+  int32_t event;           /* enum of_event */
+  int32_t stage;           /* GNC stage, 0-based */
+  int32_t level;           /* pyramid level index l (0 = finest; -1 for compute_flow_base) */
+  int32_t h, w;            /* level size */
+  int32_t iter, lin;       /* warping iteration i, linear iteration j (0-based) */
+  int32_t pad_;
+  double norm;             /* OF_EV_ITER */
+  double elapsed_s;        /* OF_EV_STAGE_END: seconds since compute_flow started */
+  const float *uv;         /* OF_EV_STAGE_END with OF_PROGRESS_FLOW, else NULL */
+} of_progress;
+typedef void (*of_progress_fn)(void *user, const of_progress *ev);
+int of_set_progress(of_ctx *ctx, of_progress_fn fn, void *user, int flags);
 /* kernel timing accumulated since enable: per kernel name total ms, launch
  * count and pixels processed (sum over launches of the level's H*W; ROF
  * counts H*W*channels); any output pointer may be NULL */
@@ -273,6 +300,14 @@ int of_pairs_submit(of_ctx *ctx, int n, const uint8_t *const *im1, const uint8_t
                     int64_t *first_ticket);
 int of_pairs_wait(of_ctx *ctx, int64_t ticket);
 int of_pairs_close(of_ctx *ctx);
+/* the same pool over device-resident pairs: queue the pairs of n slots of
+ * this context (of_pair_upload; frame size = the stream's); each flow stays
+ * in its slot (of_pair_download, of_rccl_gather_slots).  A slot must not be
+ * submitted again or re-uploaded before its ticket is waited for.  Tickets
+ * share the host submissions' sequence; flows equal of_pairs_run's with the
+ * same `lanes` bitwise (the bench's HBM-resident rate: consecutive batches
+ * queued back to back, so the lanes never drain between them). */
+int of_pairs_submit_slots(of_ctx *ctx, int n, const int *slots, int64_t *first_ticket);
 /* D2H of a slot's flow (planar 2 x H x W) */
 int of_pair_download(of_ctx *ctx, int slot, float *out_uv);
 
@@ -282,6 +317,9 @@ int of_rccl_init(of_ctx *ctx, const char *id128, int nranks, int rank);
 /* gather `nslots` flows (slots 0..nslots-1 of every rank) to rank 0; rank 0's
  * out_uv receives nranks*nslots planar flows (may be NULL on other ranks) */
 int of_rccl_gather_flows(of_ctx *ctx, int nslots, float *out_uv_rank0);
+/* the same for slots first..first+nslots-1 (rank r's slot first+s lands at
+ * flow r*nslots + s) */
+int of_rccl_gather_slots(of_ctx *ctx, int first, int nslots, float *out_uv_rank0);
 int of_rccl_finalize(of_ctx *ctx);
 
 /* ---- solver diagnostics ---- */

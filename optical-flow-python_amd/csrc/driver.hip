@@ -180,6 +180,31 @@ struct HostStage {
 #define OF_SORP_SYNC_BYTES (1024 + SOR_RING_MAX * 2 * SOR_MAXS * sizeof(int))
 #define OF_SORP_BYTES (OF_SORP_SYNC_BYTES + (SOR_RING_MAX * 2 * SOR_MAXS * 2 + SOR_RING_MAX * 2) * sizeof(double))
 
+// Streams: OF_STREAM_QUEUE=shared (env, A/B) creates plain non-blocking
+// streams, which the runtime maps onto its GPU_MAX_HW_QUEUES (4) hardware
+// queues by creation order -- after other contexts' streams came and went,
+// two busy batch lanes can land on one queue and serialise (measured: 8
+// 1080p pairs x 4 lanes, 45.7 pairs/s on a fresh context, 42.0 after a pair
+// pool's lanes were destroyed on it; tools/order_probe.py).  The default
+// gives every stream a queue of its own: a stream with a CU mask (here all
+// CUs) always gets a dedicated hardware queue.
+static void create_stream(hipStream_t *s) {
+  static const bool shared = [] {
+    const char *e = getenv("OF_STREAM_QUEUE");
+    return e && !strcmp(e, "shared");
+  }();
+  if (!shared) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0xffffffffu);
+      if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+      if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return;
+    }
+  }
+  HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+}
+
 struct of_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -212,6 +237,15 @@ struct of_ctx {
   float2 *d_sor_ring = nullptr;
   size_t sor_ring_cap = 0;  // bytes
   int sor_fallbacks = 0;    // pipelined solves rerun per sweep (hand-off timeout)
+  float *d_gather = nullptr;  // rank 0's RCCL gather receive buffer (grow-only)
+  size_t gather_cap = 0;
+  // of_set_progress: display / per-stage report callback (never on batch lanes)
+  of_progress_fn prog_fn = nullptr;
+  void *prog_user = nullptr;
+  int prog_flags = 0;
+  int prog_stage = 0, prog_level = -1;
+  std::chrono::steady_clock::time_point prog_t0;
+  std::vector<float> prog_uv;  // host copy of a stage's flow (OF_PROGRESS_FLOW)
   int opt_sor_pipe = 1;    // of_set_option(OF_OPT_SOR_PIPELINE)
   // solve log (of_set_solve_log): fp64 true residual of every solve
   int slog = 0;
@@ -1485,6 +1519,45 @@ SolveResult gen_solve_logged(of_ctx *c, const of_params *P, const GenLevel &L, c
 }
 
 // HSOpticalFlow.compute_flow_base (hs.py:109-142)
+// ---- progress reports (of_set_progress) ----
+struct ProgressOff {  // batch entries: the context (lane 0) does not report
+  of_ctx *c;
+  of_progress_fn fn;
+  explicit ProgressOff(of_ctx *c_) : c(c_), fn(c_->prog_fn) { c->prog_fn = nullptr; }
+  ~ProgressOff() { c->prog_fn = fn; }
+};
+of_progress prog_event(of_ctx *c, int event, int h, int w) {
+  of_progress e;
+  memset(&e, 0, sizeof(e));
+  e.event = event;
+  e.stage = c->prog_stage;
+  e.level = c->prog_level;
+  e.h = h;
+  e.w = w;
+  return e;
+}
+// an iteration's solve is done: ||clip(x) - d|| (d may be null) or, with
+// limit < 0, ||x|| (HS)
+void prog_iter(of_ctx *c, int it, int jl, const F2 &x, const F2 *d, int limit) {
+  if (!c->prog_fn) return;
+  of_progress e = prog_event(c, OF_EV_ITER, x.H, x.W);
+  e.iter = it;
+  e.lin = jl;
+  e.norm = std::nan("");
+  if (c->prog_flags & OF_PROGRESS_ITER) {
+    Grid2 g = grid2(x.H, x.W, PCG_MAX_BLOCKS);
+    launch(c, "step_norm2", k_step_norm2_part, g.grid, g.block, 0, (const float2 *)x.p,
+           d ? (const float2 *)d->p : (const float2 *)nullptr, limit > 0 ? 1 : 0, x.H, x.W, x.P, c->d_partials);
+    launch(c, "step_norm2", k_norm2_final, dim3(1), dim3(OF_BX, OF_BY), 0, (const double *)c->d_partials, g.nblocks,
+           c->d_norm);
+    HIPCHK(hipMemcpyAsync(c->h_norm, c->d_norm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain_solves(c);
+    e.norm = std::sqrt(*c->h_norm);
+  }
+  c->prog_fn(c->prog_user, &e);
+}
+
 void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *st) {
   const int H = L.im.H, W = L.im.W, nc = L.im.C / 2;
   c->cur_px = (double)H * W;
@@ -1499,7 +1572,14 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
     flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
     note_solve(c, st, solve_tok(c, P, coef, rhs, x));
     c->cur_px = (double)H * W;
-    if (std::sqrt(norm2(c, x)) < 1e-3) break;
+    const double xn = std::sqrt(norm2(c, x));
+    if (c->prog_fn) {  // hs.py:123-124 prints ||x|| before the exit test
+      of_progress e = prog_event(c, OF_EV_ITER, H, W);
+      e.iter = it;
+      e.norm = xn;
+      c->prog_fn(c->prog_user, &e);
+    }
+    if (xn < 1e-3) break;
     launch(c, "add_update", k_add_update, g.grid, g.block, 0, uv.p, (const float2 *)x.p, P->limit_update, H, W, uv.P);
     if (P->median_filter_size)
       for (int m = 0; m < P->mf_iter; ++m) {
@@ -1539,6 +1619,7 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
         note_solve(c, st, solve_tok(c, P, coef, rhs, x));
       }
       c->cur_px = (double)H * W;
+      prog_iter(c, it, jl, x, jl ? &duv : nullptr, P->limit_update);
       const bool filt = P->median_filter_size != 0;
       launch(c, nl && filt && L.guide.p ? "update_occ" : "update", k_update_occ, g.grid, g.block, 0,
              (const float2 *)uv.p, (const float2 *)x.p, P->limit_update, uv1.p, (const float *)L.im.p,
@@ -1598,6 +1679,7 @@ void altba_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, F2 &uvh
         note_solve(c, st, solve_tok(c, P, coef, rhs, x));
       }
       c->cur_px = (double)H * W;
+      prog_iter(c, i, jl, x, have_duv ? &duv : nullptr, P->limit_update);
       // duv = clip(x): computed as (0 + clip(x))
       HIPCHK(hipMemsetAsync(duv.p, 0, sizeof(float2) * (size_t)H * duv.P, c->stream));
       launch(c, "add_update", k_add_update, g.grid, g.block, 0, duv.p, (const float2 *)x.p, P->limit_update, H, W,
@@ -1655,6 +1737,7 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
   REQUIRE(nc >= 1 && nc <= OF_MAX_NC, OF_ENOTSUP, "1..4 channels per frame supported");
   hipEvent_t t0 = timing_event(c), t1 = timing_event(c);
   HIPCHK(hipEventRecord(t0, c->stream));
+  c->prog_t0 = std::chrono::steady_clock::now();
   // preprocessing (under the lanes' token with OF_PRE_TOKEN)
   std::unique_ptr<BigPhase> pre(new BigPhase(c, OF_PRE_TOKEN ? (double)H * W : 0.0));
   Img img;
@@ -1702,8 +1785,19 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
   for (int ig = 0; ig < gnc; ++ig) {
     const int nl = ig == 0 ? levels : P->gnc_pyramid_levels;
     const std::vector<Img> &lv = ig == 0 ? pyr : gpyr;
+    c->prog_stage = ig;
+    c->prog_level = -1;
+    if (c->prog_fn) {
+      of_progress e = prog_event(c, OF_EV_STAGE, H, W);
+      c->prog_fn(c->prog_user, &e);
+    }
     for (int l = nl - 1; l >= 0; --l) {
       const int h = lv[l].H, w = lv[l].W;
+      c->prog_level = l;
+      if (c->prog_fn) {
+        of_progress e = prog_event(c, OF_EV_LEVEL, h, w);
+        c->prog_fn(c->prog_user, &e);
+      }
       hipEvent_t e0 = timing_event(c), e1 = timing_event(c);
       HIPCHK(hipEventRecord(e0, c->stream));
       if (uv.H != h || uv.W != w) {
@@ -1734,6 +1828,20 @@ void compute_flow_dev(of_ctx *c, of_params *P, const Img &images, const Img &gui
     if (gnc > 1) {  // GNC alpha schedule (classic_nl.py:180-184, ba.py:329-333)
       const double na = 1.0 - (ig + 1.0) / (gnc - 1.0);
       P->alpha = std::max(0.0, std::min(P->alpha, na));
+    }
+    if (c->prog_fn) {  // classic_nl.py:186-196, ba.py:132-133, alt_ba.py:175-183
+      const F2 &su = P->method == OF_METHOD_ALT_BA && uvhat.p ? uvhat : uv;
+      of_progress e = prog_event(c, OF_EV_STAGE_END, su.H, su.W);
+      e.level = 0;
+      if (c->prog_flags & OF_PROGRESS_FLOW) {
+        c->prog_uv.resize(2 * (size_t)su.H * su.W);
+        download_f2(c, su, c->prog_uv.data());
+        e.uv = c->prog_uv.data();
+      }
+      HIPCHK(hipStreamSynchronize(c->stream));
+      drain_solves(c);
+      e.elapsed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->prog_t0).count();
+      c->prog_fn(c->prog_user, &e);
     }
   }
   if (P->method == OF_METHOD_BA) P->alpha = alpha_orig;  // ba.py:338-339
@@ -1866,7 +1974,7 @@ int of_ctx_create(int device, of_ctx **out) {
   c->device = device;
   try {
     HIPCHK(hipSetDevice(device));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    create_stream(&c->stream);
     HIPCHK(hipMalloc(&c->d_state, sizeof(PcgState)));
     HIPCHK(hipHostMalloc(&c->h_state, 2 * sizeof(PcgState), hipHostMallocDefault));
     HIPCHK(hipHostMalloc(&c->h_flag, OF_SOLVE_RING * sizeof(CgFlag), hipHostMallocMapped | hipHostMallocCoherent));
@@ -1920,6 +2028,7 @@ int of_ctx_destroy(of_ctx *c) {
   hipFree(c->d_sor_sync);
   if (c->d_sorp) hipFree(c->d_sorp);
   if (c->d_sor_ring) hipFree(c->d_sor_ring);
+  if (c->d_gather) hipFree(c->d_gather);
   hipFree(c->d_rpart);
   hipFree(c->d_rlog);
   hipFree(c->d_mm);
@@ -1953,6 +2062,14 @@ int of_set_option(of_ctx *c, int option, int value) {
       c->err = "unknown option";
       return OF_EINVAL;
   }
+}
+
+int of_set_progress(of_ctx *c, of_progress_fn fn, void *user, int flags) {
+  if (!c) return OF_EINVAL;
+  c->prog_fn = fn;
+  c->prog_user = user;
+  c->prog_flags = flags;
+  return OF_OK;
 }
 
 int of_get_option(of_ctx *c, int option, int64_t *value) {
@@ -2134,6 +2251,8 @@ int of_compute_flow_base(of_ctx *c, of_params *P, const float *images, int H, in
     upload_img(c, L.guide, guide);
   }
   F2 uv = upload_f2(c, uv_in, H, W);
+  c->prog_stage = 0;
+  c->prog_level = -1;
   if (P->method == OF_METHOD_HS) hs_base(c, P, L, uv, nullptr);
   else if (P->method == OF_METHOD_ALT_BA) throw OfError{OF_ENOTSUP, "AltBA compute_flow_base needs uvhat"};
   else irls_base(c, P, L, uv, alpha, P->max_linear, nullptr);
@@ -2213,6 +2332,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
           "bad arguments");
   for (int s = 0; s < nslots; ++s) REQUIRE(c->slots[s].rgb1 && c->slots[s].uv, OF_EINVAL, "slot not uploaded");
   REQUIRE(!c->pool, OF_EINVAL, "a pair stream is open on this context (of_pairs_close first)");
+  ProgressOff quiet(c);  // batch entries never report
   lanes = std::min(lanes, nslots);
   if (lanes == 1) {
     for (int s = 0; s < nslots; ++s) {
@@ -2291,7 +2411,7 @@ void stage_alloc(of_ctx *l, of_ctx *parent, size_t in_bytes, size_t out_floats) 
   if (!l->hs) {
     l->hs = new HostStage();
     if (l == parent) {
-      HIPCHK(hipStreamCreateWithFlags(&l->hs->copy, hipStreamNonBlocking));
+      create_stream(&l->hs->copy);
       l->hs->own_copy = true;
     }
     for (int b = 0; b < 2; ++b) {
@@ -2436,6 +2556,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
           OF_EINVAL, "bad arguments");
   for (int k = 0; k < npairs; ++k) REQUIRE(im1[k] && im2[k] && out_uv[k], OF_EINVAL, "null pair buffer");
   REQUIRE(!c->pool, OF_EINVAL, "a pair stream is open on this context (of_pairs_close first)");
+  ProgressOff quiet(c);  // batch entries never report
   if ((int)c->slots.size() < npairs) c->slots.resize(npairs);
   const size_t nu = 2 * (size_t)H * W;
   for (int k = 0; k < npairs; ++k) {
@@ -2517,9 +2638,11 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
 // ---- streaming batch: a persistent pool of lanes fed from a queue --------
 namespace {
 struct PairJob {
-  const uint8_t *im1, *im2;
+  const uint8_t *im1, *im2;  // host frames (of_pairs_submit) ...
   float *out;
   int64_t ticket;
+  Slot dev;                  // ... or a device-resident slot (of_pairs_submit_slots)
+  bool on_dev = false;
 };
 }  // namespace
 
@@ -2560,6 +2683,7 @@ void pool_lane(of_ctx *c, PairPool *pp, int li) {
     return true;
   };
   auto prefetch = [&](int b, const PairJob &j) {
+    if (j.on_dev) return;  // frames already in HBM
     HIPCHK(hipEventSynchronize(h.ev_in[b]));
     memcpy(h.pin_in[b], j.im1, nb);
     memcpy(h.pin_in[b] + nb, j.im2, nb);
@@ -2569,10 +2693,12 @@ void pool_lane(of_ctx *c, PairPool *pp, int li) {
   };
   auto finish = [&](int b, const PairJob &j) {
     HIPCHK(hipEventSynchronize(h.ev_conv[b]));
-    HIPCHK(hipMemcpyAsync(h.pin_out[b], duv[b], sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
-    HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
-    HIPCHK(hipEventSynchronize(h.ev_out[b]));
-    memcpy(j.out, h.pin_out[b], sizeof(float) * nu);
+    if (!j.on_dev) {  // a device slot's flow stays in its slot
+      HIPCHK(hipMemcpyAsync(h.pin_out[b], duv[b], sizeof(float) * nu, hipMemcpyDeviceToHost, h.copy));
+      HIPCHK(hipEventRecord(h.ev_out[b], h.copy));
+      HIPCHK(hipEventSynchronize(h.ev_out[b]));
+      memcpy(j.out, h.pin_out[b], sizeof(float) * nu);
+    }
     {
       std::lock_guard<std::mutex> lk(pp->m);
       pp->done[j.ticket] = 1;
@@ -2586,15 +2712,19 @@ void pool_lane(of_ctx *c, PairPool *pp, int li) {
   for (;;) {
     l->arena.reset();
     l->tev_used = 0;
-    HIPCHK(hipStreamWaitEvent(l->stream, h.ev_in[b], 0));
     Slot s;
-    s.rgb1 = h.d_in[b];
-    s.rgb2 = h.d_in[b] + nb;
-    s.u8 = true;
-    s.uv = duv[b];
-    s.H = H;
-    s.W = W;
-    s.C = C;
+    if (jobs[b].on_dev) {
+      s = jobs[b].dev;
+    } else {
+      HIPCHK(hipStreamWaitEvent(l->stream, h.ev_in[b], 0));
+      s.rgb1 = h.d_in[b];
+      s.rgb2 = h.d_in[b] + nb;
+      s.u8 = true;
+      s.uv = duv[b];
+      s.H = H;
+      s.W = W;
+      s.C = C;
+    }
     bool computed = false, got = false;
     OfError io_err{OF_OK, ""};
     std::thread io([&, b, pending] {
@@ -2727,7 +2857,60 @@ int of_pairs_submit(of_ctx *c, int n, const uint8_t *const *im1, const uint8_t *
     }
     if (first_ticket) *first_ticket = pp->next_ticket;
     for (int k = 0; k < n; ++k) {
-      pp->q.push_back({im1[k], im2[k], out_uv[k], pp->next_ticket++});
+      PairJob j;
+      j.im1 = im1[k];
+      j.im2 = im2[k];
+      j.out = out_uv[k];
+      j.ticket = pp->next_ticket++;
+      pp->q.push_back(j);
+      pp->done.push_back(0);
+    }
+  }
+  pp->cv_job.notify_all();
+  return OF_OK;
+}
+
+// queue n device-resident pairs (slots of this context, of_pair_upload); each
+// flow stays in its slot.  A slot is read and written by the lane that takes
+// it, so it must not be submitted again (or re-uploaded) before its ticket is
+// waited for.
+int of_pairs_submit_slots(of_ctx *c, int n, const int *slots, int64_t *first_ticket) {
+  if (!c) return OF_EINVAL;
+  PairPool *pp = c->pool;
+  if (!pp || n < 1 || !slots) {
+    c->err = pp ? "bad arguments" : "no pair stream open (of_pairs_open)";
+    return OF_EINVAL;
+  }
+  for (int k = 0; k < n; ++k) {
+    const int sl = slots[k];
+    if (sl < 0 || sl >= (int)c->slots.size() || !c->slots[sl].rgb1 || !c->slots[sl].uv) {
+      c->err = "slot not uploaded";
+      return OF_EINVAL;
+    }
+    if (c->slots[sl].H != pp->H || c->slots[sl].W != pp->W) {
+      c->err = "slot frame size differs from the stream's";
+      return OF_EINVAL;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(pp->m);
+    if (pp->err.code != OF_OK) {
+      c->err = pp->err.msg;
+      return pp->err.code;
+    }
+    if (pp->closing) {
+      c->err = "pair stream closing";
+      return OF_EINVAL;
+    }
+    if (first_ticket) *first_ticket = pp->next_ticket;
+    for (int k = 0; k < n; ++k) {
+      PairJob j;
+      j.im1 = j.im2 = nullptr;
+      j.out = nullptr;
+      j.ticket = pp->next_ticket++;
+      j.dev = c->slots[slots[k]];
+      j.on_dev = true;
+      pp->q.push_back(j);
       pp->done.push_back(0);
     }
   }
@@ -2813,27 +2996,42 @@ int of_rccl_init(of_ctx *c, const char *id128, int nranks, int rank) {
 }
 
 int of_rccl_gather_flows(of_ctx *c, int nslots, float *out_uv_rank0) {
+  return of_rccl_gather_slots(c, 0, nslots, out_uv_rank0);
+}
+
+int of_rccl_gather_slots(of_ctx *c, int first, int nslots, float *out_uv_rank0) {
   API_BEGIN(c)
   REQUIRE(c->comm, OF_EINVAL, "of_rccl_init first");
-  REQUIRE(nslots >= 1 && nslots <= (int)c->slots.size(), OF_EINVAL, "bad slot count");
-  const int H = c->slots[0].H, W = c->slots[0].W;
+  REQUIRE(first >= 0 && nslots >= 1 && first + nslots <= (int)c->slots.size(), OF_EINVAL, "bad slot range");
+  Slot *sl = c->slots.data() + first;
+  const int H = sl[0].H, W = sl[0].W;
   for (int s = 0; s < nslots; ++s)
-    REQUIRE(c->slots[s].uv && c->slots[s].H == H && c->slots[s].W == W, OF_EINVAL, "slots must share one size");
+    REQUIRE(sl[s].uv && sl[s].H == H && sl[s].W == W, OF_EINVAL, "slots must share one size");
   const size_t per = 2 * (size_t)H * W;
   float *recv = nullptr;
-  if (c->rank == 0) recv = (float *)c->arena.alloc(sizeof(float) * per * nslots * c->nranks);
+  if (c->rank == 0) {  // one grow-only receive buffer per context (the call ends in a sync)
+    const size_t need = sizeof(float) * per * nslots * c->nranks;
+    if (need > c->gather_cap) {
+      if (c->d_gather) HIPCHK(hipFree(c->d_gather));
+      c->d_gather = nullptr;
+      c->gather_cap = 0;
+      HIPCHK(hipMalloc(&c->d_gather, need));
+      c->gather_cap = need;
+    }
+    recv = c->d_gather;
+  }
   // rank 0's own slots first: nothing that can throw runs between
   // ncclGroupStart and ncclGroupEnd, so a failed copy cannot leave a group open
   if (c->rank == 0)
     for (int s = 0; s < nslots; ++s)
-      HIPCHK(hipMemcpyAsync(recv + per * s, c->slots[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(recv + per * s, sl[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
   ncclResult_t r = ncclGroupStart();
   for (int s = 0; s < nslots && r == ncclSuccess; ++s) {
     if (c->rank == 0) {
       for (int src = 1; src < c->nranks && r == ncclSuccess; ++src)
         r = ncclRecv(recv + per * ((size_t)src * nslots + s), per, ncclFloat, src, c->comm, c->stream);
     } else {
-      r = ncclSend(c->slots[s].uv, per, ncclFloat, 0, c->comm, c->stream);
+      r = ncclSend(sl[s].uv, per, ncclFloat, 0, c->comm, c->stream);
     }
   }
   ncclResult_t r2 = ncclGroupEnd();

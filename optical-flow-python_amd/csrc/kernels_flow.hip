@@ -443,8 +443,8 @@ __global__ void k_lo_blend(const float2 *__restrict__ u, const float2 *__restric
 // (denoise_color_weighted_medfilt2, weighted_median.py:24-112).  One wave per 8x8 tile:
 //  1. the (8+2h)^2 region is loaded straight into registers, NPER keys per
 //     lane (element e = lane*NPER + r), and guide+occ records go to LDS;
-//  2. u and v keys (order-preserving value bits << 32 | region position) are
-//     bitonic-sorted in registers; each sample's sorted index e gives it a
+//  2. u and v keys (the value widened to fp64 with the region position in
+//     its low mantissa bits, wmf_key) are bitonic-sorted in registers; each sample's sorted index e gives it a
 //     chunk id e / CH (WMF_NC chunks of CH consecutive sorted samples per list);
 //  3. every lane visits its own 15x15 window once (no out-of-window work):
 //     weight w is added to the lane's chunk sums of the u and v lists
@@ -571,21 +571,64 @@ __device__ __forceinline__ void swap_lane64(uint64_t v, int lj, uint64_t &a, uin
   b = ((uint64_t)bhi << 32) | blo;
 }
 
+// Sort keys: the flow value widened to fp64 (exact), the region position
+// (ry << 8 | rx) in the 29 mantissa bits the widening leaves zero.  As
+// doubles they order by value, ties by position (reversed for negative
+// values: any fixed tie order gives the same weighted median), -0 before +0
+// like the old integer key; +-inf and NaN map to +-2^1000 / 2^1001 (above
+// every finite fp32) so no key is a NaN, padding to 2^1002.  The position is
+// the key's low 16 bits either way.
+__device__ __forceinline__ uint64_t wmf_key(float v, unsigned pos) {
+  double d = (double)v;
+  if (__builtin_isnan(v)) d = 0x1p1001;
+  else if (__builtin_isinf(v)) d = v > 0.f ? 0x1p1000 : -0x1p1000;
+  return __builtin_bit_cast(uint64_t, d) | (uint64_t)pos;
+}
+#define WMF_PAD_KEY (__builtin_bit_cast(uint64_t, 0x1p1002) | 0xffffull)
+__device__ __forceinline__ double wmf_d(uint64_t k) { return __builtin_bit_cast(double, k); }
+// v_min_f64 / v_max_f64 without the canonicalising v_max_f64 x, x that the
+// builtins add in IEEE mode (keys are never NaN, and fp64 denormals -- the
+// keys of +-0 -- are preserved: float_denorm_mode_16_64 = 3)
+__device__ __forceinline__ uint64_t wmf_min(uint64_t a, uint64_t b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(wmf_d(a)), "v"(wmf_d(b)));
+  return __builtin_bit_cast(uint64_t, r);
+}
+__device__ __forceinline__ uint64_t wmf_max(uint64_t a, uint64_t b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(wmf_d(a)), "v"(wmf_d(b)));
+  return __builtin_bit_cast(uint64_t, r);
+}
+
 // Bitonic sort of the 64*NPER keys of two lists at once (element e = lane *
-// NPER + r).  Partners at distance >= NPER are in another lane (xor_lane64),
-// the others in the same lane.  The direction of a compare-exchange is a lane
-// mask per stage; one v_cmp_u64 + two v_cndmask per element.
+// NPER + r).  Merge kk sorts blocks of kk elements ascending where e & kk is
+// 0 and descending elsewhere; here the keys of descending blocks carry a
+// flipped sign bit during that merge (min of negated keys = max), so every
+// compare-exchange is ascending: a pair inside a lane is one v_min_f64 +
+// one v_max_f64 (was v_cmp_u64 + four v_cndmask), and only the lower lane of
+// a cross-lane pair keeps the minimum.  The sign flips between merges cost one
+// v_xor per key where the block direction changes.  Partners at distance
+// >= NPER are in another lane (xor_lane64 / v_permlane{16,32}_swap).
 template <int NPER>
 __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&kb)[NPER], int lane) {
   constexpr int N = NPER * 64;
 #pragma unroll
   for (int kk = 2; kk <= N; kk <<= 1) {
+    // sign of element e in merge kk: (e & kk) != 0; flip where it differs
+    // from merge kk/2's (no sign before the first merge)
+#pragma unroll
+    for (int r = 0; r < NPER; ++r) {
+      const int e0 = lane * NPER + r;
+      const bool s_now = (e0 & kk) != 0, s_prev = kk > 2 && (e0 & (kk >> 1)) != 0;
+      const uint64_t m = (uint64_t)(s_now != s_prev) << 63;
+      ka[r] ^= m;
+      kb[r] ^= m;
+    }
 #pragma unroll
     for (int jj = kk >> 1; jj > 0; jj >>= 1) {
       if (jj >= NPER) {
         const int lj = jj / NPER;
-        // kk > NPER here: the direction depends on the lane only
-        const bool take_min = ((lane & lj) == 0) == (((lane * NPER) & kk) == 0);
+        const bool take_min = (lane & lj) == 0;
         if (lj == 16 || lj == 32) {
           // v_permlane{16,32}_swap of a value with itself leaves (own, partner)
           // in the two outputs, in a lane-dependent order; min / max of the
@@ -595,15 +638,15 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
             uint64_t p0, p1, q0, q1;
             swap_lane64(ka[r], lj, p0, p1);
             swap_lane64(kb[r], lj, q0, q1);
-            ka[r] = ((p0 < p1) == take_min) ? p0 : p1;
-            kb[r] = ((q0 < q1) == take_min) ? q0 : q1;
+            ka[r] = ((wmf_d(p0) < wmf_d(p1)) == take_min) ? p0 : p1;
+            kb[r] = ((wmf_d(q0) < wmf_d(q1)) == take_min) ? q0 : q1;
           }
         } else {
 #pragma unroll
           for (int r = 0; r < NPER; ++r) {
             const uint64_t oa = xor_lane64(ka[r], lj), ob = xor_lane64(kb[r], lj);
-            ka[r] = ((ka[r] < oa) == take_min) ? ka[r] : oa;
-            kb[r] = ((kb[r] < ob) == take_min) ? kb[r] : ob;
+            ka[r] = ((wmf_d(ka[r]) < wmf_d(oa)) == take_min) ? ka[r] : oa;
+            kb[r] = ((wmf_d(kb[r]) < wmf_d(ob)) == take_min) ? kb[r] : ob;
           }
         }
       } else {
@@ -611,13 +654,11 @@ __device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&k
         for (int r = 0; r < NPER; ++r) {
           const int rp = r ^ jj;
           if (rp > r) {
-            const bool up = (((lane * NPER + r) & kk) == 0);
             const uint64_t a0 = ka[r], a1 = ka[rp], b0 = kb[r], b1 = kb[rp];
-            const bool sa = (a0 > a1) == up, sb = (b0 > b1) == up;
-            ka[r] = sa ? a1 : a0;
-            ka[rp] = sa ? a0 : a1;
-            kb[r] = sb ? b1 : b0;
-            kb[rp] = sb ? b0 : b1;
+            ka[r] = wmf_min(a0, a1);
+            ka[rp] = wmf_max(a0, a1);
+            kb[r] = wmf_min(b0, b1);
+            kb[rp] = wmf_max(b0, b1);
           }
         }
       }
@@ -671,15 +712,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
   for (int r = 0; r < NPER; ++r) {
     const int s = lane * NPER + r;
-    a[r] = ~0ull;
-    b[r] = ~0ull;
+    a[r] = WMF_PAD_KEY;
+    b[r] = WMF_PAD_KEY;
     if (s < nreg) {
       const int ry = s / RW, rx = s - ry * RW;
       const size_t g = (size_t)mir(ty0 - hsz + ry, H) * P + mir(tx0 - hsz + rx, W);
       const float2 v = uv[g];
-      const uint64_t lo = ((uint64_t)ry << 8) | (uint64_t)rx;
-      a[r] = ((uint64_t)f2ord(v.x) << 32) | lo;
-      b[r] = ((uint64_t)f2ord(v.y) << 32) | lo;
+      const unsigned lo = ((unsigned)ry << 8) | (unsigned)rx;
+      a[r] = wmf_key(v.x, lo);
+      b[r] = wmf_key(v.y, lo);
       float gv[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < GC; ++c) gv[c] = guide[c * ps + g];
@@ -778,35 +819,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   if (chv < 0) { chv = lastv; bv = lbv; }
   WMF_STAMP(4);
   const unsigned span = 2u * hsz;
+  // walk results as record indices relative to the lane's window origin qb
+  // (0xffff: none yet)
   unsigned resu = 0xffffu, resv = 0xffffu, lstu = 0, lstv = 0;
-  // the crossing chunks' sorted positions, 8 per 16-B read
+  // the crossing chunks' sorted positions (ry << 8 | rx), 8 per 16-B read;
+  // window offsets straight from the position bytes (dy = ry - py and
+  // dx = rx - px as unsigned: out of the window unless both <= span; padding
+  // keys have ry = 255)
   const uint4 *wu = reinterpret_cast<const uint4 *>(ku + chu * CH), *wv = reinterpret_cast<const uint4 *>(kv + chv * CH);
   for (int g = 0; g < CH / 8; ++g) {
     const uint4 A = wu[g], B = wv[g];
     const unsigned wa4[4] = {A.x, A.y, A.z, A.w}, wb4[4] = {B.x, B.y, B.z, B.w};
-    unsigned ka[8], kb[8];
+    unsigned qa[8], qv[8];
     bool ina[8], inb[8];
     T ra[8], rb[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      ka[i] = (wa4[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      kb[i] = (wb4[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      const unsigned rya = ka[i] >> 8, rxa = ka[i] & 0xffu, ryb = kb[i] >> 8, rxb = kb[i] & 0xffu;
-      // padding keys (0xffff) fail the window test (ry = 255)
-      ina[i] = (rya - (unsigned)py) <= span && (rxa - (unsigned)px) <= span;
-      inb[i] = (ryb - (unsigned)py) <= span && (rxb - (unsigned)px) <= span;
-      ra[i] = smp[ina[i] ? rya * RP + rxa : 0u];
-      rb[i] = smp[inb[i] ? ryb * RP + rxb : 0u];
+      const int sh = 16 * (i & 1);
+      const unsigned wa = wa4[i >> 1], wb = wb4[i >> 1];
+      const unsigned dya = ((wa >> (sh + 8)) & 0xffu) - (unsigned)py, dxa = ((wa >> sh) & 0xffu) - (unsigned)px;
+      const unsigned dyb = ((wb >> (sh + 8)) & 0xffu) - (unsigned)py, dxb = ((wb >> sh) & 0xffu) - (unsigned)px;
+      ina[i] = max(dya, dxa) <= span;
+      inb[i] = max(dyb, dxb) <= span;
+      qa[i] = ina[i] ? dya * (unsigned)RP + dxa : 0u;
+      qv[i] = inb[i] ? dyb * (unsigned)RP + dxb : 0u;
+      ra[i] = smp[qb + qa[i]];
+      rb[i] = smp[qb + qv[i]];
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float xa = wmf_w(ra[i], c01, cg[2], nk), xb = wmf_w(rb[i], c01, cg[2], nk);
-      bu += ina[i] ? (double)xa : 0.0;
-      bv += inb[i] ? (double)xb : 0.0;
-      resu = (resu == 0xffffu && ina[i] && bu >= half) ? ka[i] : resu;
-      resv = (resv == 0xffffu && inb[i] && bv >= half) ? kb[i] : resv;
-      lstu = ina[i] ? ka[i] : lstu;
-      lstv = inb[i] ? kb[i] : lstv;
+      bu += (double)(ina[i] ? xa : 0.f);  // select before the widening: one v_cndmask
+      bv += (double)(inb[i] ? xb : 0.f);
+      resu = (resu == 0xffffu && ina[i] && bu >= half) ? qa[i] : resu;
+      resv = (resv == 0xffffu && inb[i] && bv >= half) ? qv[i] : resv;
+      lstu = ina[i] ? qa[i] : lstu;
+      lstv = inb[i] ? qv[i] : lstv;
     }
   }
   if (resu == 0xffffu) resu = lstu;
@@ -814,8 +862,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   WMF_STAMP(5);
   if (gi < H && gj < W) {
     // the selected samples' values, re-read at their (mirrored) positions
-    const int ya = mir(ty0 - hsz + (int)(resu >> 8), H), xa = mir(tx0 - hsz + (int)(resu & 0xffu), W);
-    const int yb = mir(ty0 - hsz + (int)(resv >> 8), H), xb = mir(tx0 - hsz + (int)(resv & 0xffu), W);
+    const int dya = (int)(resu / (unsigned)RP), dyb = (int)(resv / (unsigned)RP);
+    const int ya = mir(gi - hsz + dya, H), xa = mir(gj - hsz + (int)resu - dya * RP, W);
+    const int yb = mir(gi - hsz + dyb, H), xb = mir(gj - hsz + (int)resv - dyb * RP, W);
     float2 med = make_float2(uv[(size_t)ya * P + xa].x, uv[(size_t)yb * P + xb].y);
     if (base) {  // out = base + (med - base): classic_nl.py:271-275 fused (out may alias base)
       const float2 b0 = base[(size_t)gi * P + gj];

@@ -2167,6 +2167,23 @@ __global__ __launch_bounds__(256) void k_norm2_part(const float2 *__restrict__ x
   }
   write_partials<1>(v, part, lds);
 }
+// sum of squares of clip(x) - d (d may be null; clip to [-1, 1] when limit):
+// the reference's display norm ||x - duv|| (classic_nl.py:255-256,
+// ba.py:189-190, alt_ba.py:249-250), partials for k_norm2_final
+__global__ __launch_bounds__(256) void k_step_norm2_part(const float2 *__restrict__ x, const float2 *__restrict__ d,
+                                                         int limit, int H, int W, int P, double *part) {
+  __shared__ double lds[32];
+  double v[1] = {0.0};
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    float2 a = x[k];
+    if (limit) a = make_float2(fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f));
+    const double u = (double)a.x - (d ? (double)d[k].x : 0.0), w = (double)a.y - (d ? (double)d[k].y : 0.0);
+    v[0] += u * u + w * w;
+  }
+  write_partials<1>(v, part, lds);
+}
 __global__ __launch_bounds__(256) void k_norm2_final(const double *part, int nb, double *result) {
   __shared__ double lds[32];
   double s[1];

@@ -90,6 +90,20 @@ class OfStats(C.Structure):
         }
 
 
+# of_set_progress (include/optflow.h): events and flags
+OF_EV_STAGE, OF_EV_LEVEL, OF_EV_ITER, OF_EV_STAGE_END = 0, 1, 2, 3
+OF_PROGRESS_ITER, OF_PROGRESS_FLOW = 1, 2
+
+
+class OfProgress(C.Structure):
+    _fields_ = [("event", C.c_int32), ("stage", C.c_int32), ("level", C.c_int32), ("h", C.c_int32),
+                ("w", C.c_int32), ("iter", C.c_int32), ("lin", C.c_int32), ("pad_", C.c_int32),
+                ("norm", C.c_double), ("elapsed_s", C.c_double), ("uv", C.POINTER(C.c_float))]
+
+
+OfProgressFn = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(OfProgress))
+
+
 class OfCgGeometry(C.Structure):
     _fields_ = [("grid_x", C.c_int32), ("grid_y", C.c_int32), ("rows", C.c_int32), ("bands", C.c_int32),
                 ("blocks", C.c_int32), ("strip_cols", C.c_int32)]

@@ -10,8 +10,8 @@ import threading
 
 import numpy as np
 
-from optical_flow._abi import (OfParams, OfStats, OfCgGeometry, OfSolveRecord, OF_ABI_VERSION, OF_EINVAL,
-                               OF_ENOTSUP)
+from optical_flow._abi import (OfParams, OfStats, OfCgGeometry, OfSolveRecord, OfProgressFn, OF_ABI_VERSION,
+                               OF_EINVAL, OF_ENOTSUP)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OPTFLOW_LIB", os.path.join(_HERE, "_lib", "liboptflow.so"))
@@ -35,6 +35,7 @@ _SIGS = {
     "of_set_profiling": ([_vp, C.c_int], C.c_int),
     "of_set_option": ([_vp, C.c_int, C.c_int], C.c_int),
     "of_get_option": ([_vp, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "of_set_progress": ([_vp, OfProgressFn, _vp, C.c_int], C.c_int),
     "of_kernel_times": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, C.POINTER(C.c_int64), _dp, _ip], C.c_int),
     "of_kernel_timeline": ([_vp, C.c_int, C.POINTER(C.c_char_p), _dp, _dp, _dp, _ip], C.c_int),
     "of_estimate_flow": ([_vp, C.POINTER(OfParams), _fp, _fp, C.c_int, C.c_int, C.c_int, _fp, _fp,
@@ -55,10 +56,12 @@ _SIGS = {
     "of_pairs_submit": ([_vp, C.c_int, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(C.c_int64)],
                         C.c_int),
     "of_pairs_wait": ([_vp, C.c_int64], C.c_int),
+    "of_pairs_submit_slots": ([_vp, C.c_int, _ip, C.POINTER(C.c_int64)], C.c_int),
     "of_pairs_close": ([_vp], C.c_int),
     "of_rccl_unique_id": ([C.c_char_p], C.c_int),
     "of_rccl_init": ([_vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
     "of_rccl_gather_flows": ([_vp, C.c_int, _fp], C.c_int),
+    "of_rccl_gather_slots": ([_vp, C.c_int, C.c_int, _fp], C.c_int),
     "of_rccl_finalize": ([_vp], C.c_int),
     "of_preprocess": ([_vp, _fp, _fp, C.c_int, C.c_int, _fp, _fp], C.c_int),
     "of_rof_texture": ([_vp, _fp, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double, _fp], C.c_int),
@@ -144,6 +147,22 @@ class Context:
         v = C.c_int64(0)
         self.check(self.lib.of_get_option(self.handle, int(option), C.byref(v)))
         return v.value
+
+    def progress(self, fn, flags):
+        """Context manager: of_set_progress(fn, flags) for the calls inside it
+        (fn(OfProgress) -> None; see include/optflow.h), NULL afterwards."""
+        ctx = self
+
+        class _P:
+            def __enter__(self):
+                self.cb = OfProgressFn(lambda user, ev: fn(ev.contents))
+                ctx.check(ctx.lib.of_set_progress(ctx.handle, self.cb, None, int(flags)))
+                return self
+
+            def __exit__(self, *exc):
+                ctx.lib.of_set_progress(ctx.handle, OfProgressFn(), None, 0)
+                return False
+        return _P()
 
     def set_solve_log(self, enable=True):
         """Log the fp64 true residual of every linear solve (of_set_solve_log)."""

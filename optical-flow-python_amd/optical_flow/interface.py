@@ -9,11 +9,15 @@ import numpy as np
 
 from optical_flow import _abi
 from optical_flow import _native as nat
+from optical_flow.methods.base import progress_printer
 from optical_flow.methods.config import load_of_method
 
 
-def estimate_flow(im1, im2, method='classic+nl-fast', params=None):
-    """Flow (H, W, 2) float64 from im1 to im2; (H, W) or (H, W, >=3) inputs."""
+def estimate_flow(im1, im2, method='classic+nl-fast', params=None, gt=None):
+    """Flow (H, W, 2) float64 from im1 to im2; (H, W) or (H, W, >=3) inputs.
+    Prints what the reference's compute_flow prints.  `gt` (an extension:
+    the reference's estimate_flow has no such argument) is handed to the
+    per-GNC-stage report as compute_flow(init, gt) would get it."""
     im1 = np.asarray(im1, dtype=float)
     im2 = np.asarray(im2, dtype=float)
     ope = load_of_method(method)
@@ -25,7 +29,7 @@ def estimate_flow(im1, im2, method='classic+nl-fast', params=None):
         ope.images = np.concatenate([im1, im2], axis=2)
         if ope.color_images is not None:
             ope.color_images = im1.copy()
-        return ope.compute_flow(np.zeros((H, W, 2)))
+        return ope.compute_flow(np.zeros((H, W, 2)), gt)
     if im1.ndim == 3:
         a = nat.f32(im1[:, :, :3])
         b = nat.f32(im2[:, :, :3])
@@ -37,8 +41,10 @@ def estimate_flow(im1, im2, method='classic+nl-fast', params=None):
     out = np.empty((2, H, W), dtype=np.float32)
     st = _abi.OfStats()
     ctx = nat.context()
-    ctx.check(ctx.lib.of_estimate_flow(ctx.handle, C.byref(P), nat.ptr(a), nat.ptr(b), H, W, Cc, None,
-                                       nat.ptr(out), C.byref(st)))
+    fn, flags = progress_printer(ope, gt)  # the reference's compute_flow prints (interface.py:66)
+    with ctx.progress(fn, flags):
+        ctx.check(ctx.lib.of_estimate_flow(ctx.handle, C.byref(P), nat.ptr(a), nat.ptr(b), H, W, Cc, None,
+                                           nat.ptr(out), C.byref(st)))
     ope.alpha = P.alpha
     ope.last_stats = st.as_dict()
     return nat.interleaved(out)

@@ -6,7 +6,7 @@ import numpy as np
 
 from optical_flow import _abi
 from optical_flow import _native as nat
-from optical_flow.methods.base import BaseOpticalFlow
+from optical_flow.methods.base import BaseOpticalFlow, progress_printer
 from optical_flow.robust.robust_function import RobustFunction
 
 
@@ -68,7 +68,10 @@ class AltBAOpticalFlow(BaseOpticalFlow):
         out_uv = np.empty((2, H, W), dtype=np.float32)
         out_hat = np.empty((2, H, W), dtype=np.float32)
         ctx = nat.context()
-        ctx.check(ctx.lib.of_alt_ba_flow_base(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc, float(self.alpha),
-                                              int(bool(self.replacement)), nat.ptr(nat.planar(uv)),
-                                              nat.ptr(nat.planar(uvhat)), nat.ptr(out_uv), nat.ptr(out_hat)))
+        fn, flags = progress_printer(self, None)
+        with ctx.progress(fn, flags):
+            ctx.check(ctx.lib.of_alt_ba_flow_base(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc,
+                                                  float(self.alpha), int(bool(self.replacement)),
+                                                  nat.ptr(nat.planar(uv)), nat.ptr(nat.planar(uvhat)),
+                                                  nat.ptr(out_uv), nat.ptr(out_hat)))
         return nat.interleaved(out_uv), nat.interleaved(out_hat)

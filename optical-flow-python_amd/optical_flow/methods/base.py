@@ -6,7 +6,6 @@ compute_flow / compute_flow_base / flow_operator / _solve_linear_system run
 on the GPU through liboptflow.so (include/optflow.h); there is no CPU path.
 """
 import ctypes as C
-import time
 from abc import ABC
 
 import numpy as np
@@ -17,6 +16,51 @@ from optical_flow import _native as nat
 from optical_flow.robust.robust_function import RobustFunction
 
 _DEFAULT_FILTERS = (np.array([[1, -1]]), np.array([[1], [-1]]))
+
+
+def progress_printer(ope, gt):
+    """(callback, of_set_progress flags) printing what the reference's
+    compute_flow prints for `ope`: with ope.display the GNC stage / pyramid
+    level headers and each iteration's ||x - duv|| (HS: ||x||)
+    (classic_nl.py:141-152, 255-256; ba.py:101-114, 189-190; hs.py:80-81,
+    123-124; alt_ba.py:128-139, 249-250), and after every GNC stage (always,
+    not for HS) "GNC stage k finished, m minutes passed", with `gt` the
+    stage's AAE / STD / EPE (classic_nl.py:186-196; alt_ba.py:175-183 prints
+    them on a line of their own; ba.py:132-133 has none)."""
+    meth = ope._METHOD
+    display = bool(getattr(ope, 'display', False))
+    want_flow = gt is not None and meth in ('classic_nl', 'alt_ba')
+    flags = (_abi.OF_PROGRESS_ITER if display else 0) | (_abi.OF_PROGRESS_FLOW if want_flow else 0)
+
+    def fn(e):
+        if e.event == _abi.OF_EV_STAGE:
+            if display and meth != 'hs':
+                print(f"GNC stage: {e.stage + 1}")
+        elif e.event == _abi.OF_EV_LEVEL:
+            if display:
+                print(f"Pyramid level: {e.level + 1}" if meth == 'hs' else f"  Pyramid level: {e.level + 1}")
+        elif e.event == _abi.OF_EV_ITER:
+            if display:
+                if meth == 'hs':
+                    print(f"  Iteration: {e.iter + 1}  (norm: {e.norm:.6f})")
+                else:
+                    print(f"    Iter: {e.iter + 1} {e.lin + 1} (delta: {e.norm:.6f})")
+        elif e.event == _abi.OF_EV_STAGE_END and meth != 'hs':
+            msg = f"GNC stage {e.stage + 1} finished, {e.elapsed_s / 60:.2f} minutes passed"
+            extra = None
+            if want_flow and e.uv:
+                from optical_flow.evaluation.metrics import flow_angular_error
+                uv = np.ctypeslib.as_array(e.uv, shape=(2, e.h, e.w)).astype(np.float64)
+                g = np.asarray(gt, dtype=float)
+                if g.shape[:2] == (e.h, e.w):
+                    aae, stdae, aepe = flow_angular_error(g[:, :, 0], g[:, :, 1], uv[0], uv[1], 0)
+                    extra = f"AAE {aae:.3f} STD {stdae:.3f} EPE {aepe:.3f}"
+            if extra and meth == 'classic_nl':
+                msg += "  " + extra
+            print(msg)
+            if extra and meth == 'alt_ba':
+                print("  " + extra)
+    return fn, flags
 
 
 class BaseOpticalFlow(ABC):
@@ -240,7 +284,9 @@ class BaseOpticalFlow(ABC):
 
     def compute_flow(self, init=None, gt=None):
         """GNC x coarse-to-fine x IRLS on the GPU (hs.py:49-99, ba.py:57-138,
-        classic_nl.py:89-198, alt_ba.py:81-187)."""
+        classic_nl.py:89-198, alt_ba.py:81-187).  Prints what the reference
+        prints (display lines, the per-GNC-stage report with AAE/STD/EPE
+        against `gt`) from the library's progress events (of_set_progress)."""
         images, H, W, nc = self._images_planar()
         guide, gc = self._guide_planar(H, W)
         P = self.to_params()
@@ -248,27 +294,15 @@ class BaseOpticalFlow(ABC):
         out = np.empty((2, H, W), dtype=np.float32)
         st = _abi.OfStats()
         ctx = nat.context()
-        t0 = time.time()
-        ctx.check(ctx.lib.of_compute_flow(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc,
-                                          nat.ptr(guide), gc, nat.ptr(init_p), nat.ptr(out), C.byref(st)))
+        fn, flags = progress_printer(self, gt)
+        with ctx.progress(fn, flags):
+            ctx.check(ctx.lib.of_compute_flow(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc,
+                                              nat.ptr(guide), gc, nat.ptr(init_p), nat.ptr(out), C.byref(st)))
         self.alpha = P.alpha
         if self._METHOD in ('hs', 'alt_ba') or getattr(self, 'auto_level', False):
             self.pyramid_levels = P.pyramid_levels
         self.last_stats = st.as_dict()
-        uv = nat.interleaved(out)
-        self._report(gt, uv, time.time() - t0)
-        return uv
-
-    def _report(self, gt, uv, seconds):
-        if self._METHOD == 'hs' and gt is None:
-            return
-        msg = f"GNC stages finished, {seconds / 60:.2f} minutes passed"
-        if gt is not None:
-            from optical_flow.evaluation.metrics import flow_angular_error
-            aae, stdae, aepe = flow_angular_error(gt[:, :, 0], gt[:, :, 1], uv[:, :, 0], uv[:, :, 1], 0)
-            msg += f"  AAE {aae:.3f} STD {stdae:.3f} EPE {aepe:.3f}"
-        if self.display or gt is not None:
-            print(msg)
+        return nat.interleaved(out)
 
     def compute_flow_base(self, uv):
         """One pyramid level (hs.py:109-142, ba.py:143-206, classic_nl.py:200-277)
@@ -279,8 +313,10 @@ class BaseOpticalFlow(ABC):
         uvp = nat.planar(uv)
         out = np.empty((2, H, W), dtype=np.float32)
         ctx = nat.context()
-        ctx.check(ctx.lib.of_compute_flow_base(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc, nat.ptr(guide),
-                                               gc, float(self.alpha), nat.ptr(uvp), nat.ptr(out)))
+        fn, flags = progress_printer(self, None)
+        with ctx.progress(fn, flags):
+            ctx.check(ctx.lib.of_compute_flow_base(ctx.handle, C.byref(P), nat.ptr(images), H, W, nc,
+                                                   nat.ptr(guide), gc, float(self.alpha), nat.ptr(uvp), nat.ptr(out)))
         return nat.interleaved(out)
 
     def _operator_planes(self, uv, duv, It, Ix, Iy, alpha):

@@ -642,6 +642,46 @@ def gen_chaos_synth():
     save("chaos_synth.npz", **out)
 
 
+def _printed(fn, *a, **k):
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        fn(*a, **k)
+    return buf.getvalue().splitlines()
+
+
+def gen_display():
+    """The reference's printed output (display lines, per-GNC-stage report)
+    for estimate_flow on the e2e_small crop and, with a ground truth passed to
+    compute_flow, on synth_pair(48, 64, 3): display.json {case: [lines]}."""
+    import json
+    from optical_flow.methods.classic_nl import ClassicNLOpticalFlow
+    from optical_flow.methods.alt_ba import AltBAOpticalFlow
+    im1, im2 = rubberwhale()
+    c1 = im1[150:198, 250:314].copy()
+    c2 = im2[150:198, 250:314].copy()
+    out = {}
+    for m in ("classic+nl-fast", "hs", "ba", "classic-c"):
+        out[m] = _printed(ref.estimate_flow, c1, c2, m)
+    s1, s2, gt = synthetic.synth_pair(48, 64, 3)
+    out["gt"] = gt.tolist()
+    for cls, m, params in ((ClassicNLOpticalFlow, "classic+nl-fast", None),
+                           (AltBAOpticalFlow, "classic-c-a", {"lambda2": 0.01})):
+        orig = cls.compute_flow
+        cls.compute_flow = lambda self, init=None, gt_=None, _o=orig: _o(self, init, gt)
+        try:
+            out["gt:" + m] = _printed(ref.estimate_flow, s1, s2, m, params)
+        finally:
+            cls.compute_flow = orig
+    out["synth"] = {"im1": s1.tolist(), "im2": s2.tolist()}
+    path = os.path.join(HERE, "display.json")
+    with open(path, "w") as f:
+        json.dump(out, f)
+    print(f"wrote display.json ({os.path.getsize(path)/1024:.1f} KiB)")
+    for k, v in out.items():
+        if isinstance(v, list) and v and isinstance(v[0], str):
+            print(k, len(v), v[:6])
+
+
 if __name__ == "__main__":
     jobs = sys.argv[1:] or ["unit", "e2e_small", "e2e_synth"]
     for j in jobs:

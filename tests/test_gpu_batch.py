@@ -84,6 +84,68 @@ def test_pairs_run_lanes_bitwise():
     ctx.close()
 
 
+def test_pairs_submit_slots_matches_pairs_run():
+    """The pair pool over device-resident slots (of_pairs_submit_slots, the
+    bench's timed form): two sets of slots queued back to back, host pairs
+    interleaved in the same pool, waited out of order -- every slot's flow is
+    bitwise of_pairs_run's with the same lanes, the host pairs' flows equal
+    of_pairs_run_host's; bad slots raise."""
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    lib = ctx.lib
+    H, W, n, lanes = 60, 88, 3, 2
+    frames = [synth_pair(H, W, 40 + s)[:2] for s in range(n)]
+    for k in range(2):
+        for s, (a, b) in enumerate(frames):
+            ctx.check(lib.of_pair_upload(ctx.handle, k * n + s, _native.ptr(_native.f32(a)),
+                                         _native.ptr(_native.f32(b)), H, W, 3))
+    P0 = _params("classic+nl-fast")
+    ctx.check(lib.of_pairs_run(ctx.handle, n, C.byref(P0), lanes, None))
+    ref = np.empty((n, 2, H, W), np.float32)
+    for s in range(n):
+        ctx.check(lib.of_pair_download(ctx.handle, s, _native.ptr(ref[s])))
+    u8 = [(np.ascontiguousarray(a.astype(np.uint8)), np.ascontiguousarray(b.astype(np.uint8))) for a, b in frames]
+    hout = [np.empty((2, H, W), np.float32) for _ in range(n)]
+    vp = C.c_void_p
+    p1 = (vp * n)(*[x[0].ctypes.data for x in u8])
+    p2 = (vp * n)(*[x[1].ctypes.data for x in u8])
+    po = (vp * n)(*[o.ctypes.data for o in hout])
+    hwant = [np.empty((2, H, W), np.float32) for _ in range(n)]
+    pw = (vp * n)(*[o.ctypes.data for o in hwant])
+    ctx.check(lib.of_pairs_run_host(ctx.handle, n, p1, p2, H, W, 3, C.byref(P0), lanes, pw, None))
+    # of_pairs_run_host released the slots' frames: upload both sets again
+    for k in range(2):
+        for s, (a, b) in enumerate(frames):
+            ctx.check(lib.of_pair_upload(ctx.handle, k * n + s, _native.ptr(_native.f32(a)),
+                                         _native.ptr(_native.f32(b)), H, W, 3))
+    ctx.check(lib.of_pairs_open(ctx.handle, H, W, 3, C.byref(P0), lanes))
+    try:
+        t = []
+        for k in range(2):
+            first = C.c_int64(0)
+            ctx.check(lib.of_pairs_submit_slots(ctx.handle, n, (C.c_int * n)(*range(k * n, (k + 1) * n)),
+                                                C.byref(first)))
+            t.append(first.value)
+        th = C.c_int64(0)
+        ctx.check(lib.of_pairs_submit(ctx.handle, n, p1, p2, po, C.byref(th)))
+        for tk in [t[1] + 2, t[0], th.value + 1, t[1], t[0] + 1, th.value, t[1] + 1, t[0] + 2, th.value + 2]:
+            ctx.check(lib.of_pairs_wait(ctx.handle, tk))
+        with pytest.raises(ValueError):
+            ctx.check(lib.of_pairs_submit_slots(ctx.handle, 1, (C.c_int * 1)(2 * n + 3), None))
+    finally:
+        ctx.check(lib.of_pairs_close(ctx.handle))
+    for k in range(2):
+        for s in range(n):
+            uv = np.empty((2, H, W), np.float32)
+            ctx.check(lib.of_pair_download(ctx.handle, k * n + s, _native.ptr(uv)))
+            np.testing.assert_array_equal(uv, ref[s], err_msg=f"set {k} slot {s}")
+    for s in range(n):
+        np.testing.assert_array_equal(hout[s], hwant[s])
+        np.testing.assert_array_equal(hwant[s], ref[s])
+    ctx.close()
+
+
 def test_rccl_gather_single_rank():
     from optical_flow import _native
     from optical_flow.utils.synthetic import synth_pair
@@ -105,8 +167,13 @@ def test_rccl_gather_single_rank():
             uv = np.empty((2, H, W), np.float32)
             ctx.check(lib.of_pair_download(ctx.handle, s, _native.ptr(uv)))
             np.testing.assert_array_equal(out[s], uv)
+        out1 = np.full((1, 2, H, W), np.nan, np.float32)
+        ctx.check(lib.of_rccl_gather_slots(ctx.handle, 1, 1, _native.ptr(out1)))
+        np.testing.assert_array_equal(out1[0], out[1])
         with pytest.raises(ValueError):
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, 5, None))  # more slots than uploaded
+        with pytest.raises(ValueError):
+            ctx.check(lib.of_rccl_gather_slots(ctx.handle, 1, 2, None))
     finally:
         lib.of_rccl_finalize(ctx.handle)
         ctx.close()

@@ -8,7 +8,7 @@ TAG=$1; A=$2; B=$3
 export PYTHONDONTWRITEBYTECODE=1
 O=gpurun_out/$TAG; mkdir -p $O
 tools/gpu_step.sh 300 $O/wmf_tests.log python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_gpu_stages.py tests/test_gpu_e2e.py -k "weighted_median or wmf or nl-fast or rubberwhale" || exit $?
+  tests/test_gpu_batch.py tests/test_gpu_stages.py tests/test_gpu_e2e.py -k "batch or pairs or slot or rccl or weighted_median or wmf or nl-fast or rubberwhale" || exit $?
 grep -q " passed" $O/wmf_tests.log && ! grep -q " failed" $O/wmf_tests.log || { echo "WMF tests failed"; exit 1; }
 for rep in 1 2 3; do for L in $A $B; do
   tools/gpu_step.sh 120 $O/wmf_bench_tmp.log python -u tools/wmf_bench.py --lib $L --reps 20 || exit $?
