@@ -58,6 +58,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 KERNEL_BYTES_PER_PX = {
     "pcg_iter": 8 + 8 + 8 + 28 + 3 * 8,    # fused CG iteration: r, x, p_old + 7 coef planes -> r, x, p_new
     "flow_operator": 8 + 12 + 28 + 8,      # uv, It/Ix/Iy -> 7 coef + rhs
+    # warp + derivatives + assembly fused (nc = 1): uv, I1, I2/DX/DY/DXY (Hermite;
+    # 3 planes for the B-spline / bilinear forms), I1x, I1y -> 7 coef + rhs
+    "warp_operator_hermite": 8 + 4 + 4 * 4 + 8 + 36,
+    "warp_operator_bspline": 8 + 4 + 3 * 4 + 8 + 36,
+    "warp_operator_bilinear": 8 + 4 + 3 * 4 + 8 + 36,
     "partial_deriv_hermite": 8 + 4 * 4 + 3 * 4 + 12,  # uv, I2/DX/DY/DXY, I1/I1x/I1y -> It/Ix/Iy
     "update_occ": 16 + 8 + 8 + 4,          # uv, x, I1, I2 -> uv1, occ
     "wmf": 8 + 4 + 12 + 8,                 # uv, occ, Lab -> uv
@@ -336,7 +341,10 @@ def profiled_replay(ctx, lib, P0, pairs, lanes, timeline=None):
 # N (48 warp+derivatives + 56 weights/assembly + 24 update/clip) + 76 N K_pcg
 # bytes, over the time of every kernel of the loop
 INNER_BYTES = {"partial_deriv_hermite": 48, "partial_deriv_bspline": 44, "partial_deriv_bilinear": 44,
-               "flow_operator": 56, "update_occ": 24}
+               "flow_operator": 56, "update_occ": 24,
+               # the fused warp + assembly: its compulsory I/O (the It/Ix/Iy
+               # round trip of the two-kernel form is gone)
+               "warp_operator_hermite": 72, "warp_operator_bspline": 68, "warp_operator_bilinear": 68}
 INNER_TIME_ONLY = ("pcg_small", "pcg_check", "cg_update", "cg_finalize", "axpy_diff", "add_update", "sor_init",
                    "sor_final")
 
@@ -370,8 +378,8 @@ def inner_loop_of(ktimes, per_level):
     fine = max((px for (n, px) in per_level if n in ("pcg_iter", "sor_sweep", "sor_pipe")), default=None)
     out = {"bytes_per_step": round(byt), "kernel_ms_per_step": round(ms, 3), "achieved": round(ach, 1),
            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-           "formula": "sum N*(48|44 + 56 + 24) per warp + 76*N*K_pcg | 52*N*K_sor; time of warp, assembly, update, "
-                      "solver kernels"}
+           "formula": "sum N*(48|44 + 56 + 24) per warp (fused warp + assembly: N*(72|68 + 24)) + 76*N*K_pcg | "
+                      "52*N*K_sor; time of warp, assembly, update, solver kernels"}
     if fine:
         b2 = sum(INNER_BYTES[n] * r["px"] for (n, px), r in per_level.items() if px == fine and n in INNER_BYTES)
         b2 += KERNEL_BYTES_PER_PX["pcg_iter"] * per_level.get(("pcg_iter.active", fine), {"px": 0})["px"]

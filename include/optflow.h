@@ -172,6 +172,12 @@ int of_set_profiling(of_ctx *ctx, int enable);
  *                        sweep (k_sor_lex).  Both give the same iterate and
  *                        sweep count bitwise. */
 #define OF_OPT_SOR_PIPELINE 1
+/*   OF_OPT_FUSED_WARP    1 (default): each warping iteration's partial_deriv
+ *                        and flow_operator run as one kernel (no It / Ix /
+ *                        Iy planes; 1 or 3 channels, one linearisation per
+ *                        warp); 0: two kernels.  The same system either way
+ *                        (tests/test_gpu_stages.py). */
+#define OF_OPT_FUSED_WARP 3
 int of_set_option(of_ctx *ctx, int option, int value);
 /* read an option, or a read-only counter of the context and its batch lanes:
  *   OF_OPT_SOR_FALLBACKS  pipelined SOR solves whose sweep hand-off timed out

@@ -53,19 +53,27 @@ __host__ static inline PenF to_penf(const of_penalty &p) {
   return q;
 }
 
+// rho'(x)/x per kind (penalties.py d_type == 2); pen_k<K> picks one at
+// compile time (the assembly kernels specialised on the method's penalty
+// kinds), pen_w at run time -- the same arithmetic either way
+__device__ __forceinline__ float pen_quad(const PenF &p, float) { return 2.0f / (p.p0 * p.p0); }
+__device__ __forceinline__ float pen_lorentz(const PenF &p, float x) { return 2.0f / (2.0f * p.p0 * p.p0 + x * x); }
+__device__ __forceinline__ float pen_charb(const PenF &p, float x) {
+  float s2 = p.p0 * p.p0, t = x / s2;
+  return 1.0f / (s2 * sqrtf(1.0f + t * t));
+}
+// (sigma^2 + x^2)^(a-1) as exp2((a-1) log2(.)): the base is a normal
+// positive float (sigma^2 + x^2 >= sigma^2), so the hardware v_log_f32 /
+// v_exp_f32 pair (~1 ulp each) replaces the ~30-instruction general powf
+__device__ __forceinline__ float pen_gcharb(const PenF &p, float x) {
+  return 2.0f * p.p1 * __builtin_amdgcn_exp2f((p.p1 - 1.0f) * __builtin_amdgcn_logf(p.p0 * p.p0 + x * x));
+}
 __device__ __forceinline__ float pen_w(const PenF &p, float x) {
   switch (p.kind) {
-    case OF_PEN_QUADRATIC: return 2.0f / (p.p0 * p.p0);
-    case OF_PEN_LORENTZIAN: return 2.0f / (2.0f * p.p0 * p.p0 + x * x);
-    case OF_PEN_CHARBONNIER: {
-      float s2 = p.p0 * p.p0, t = x / s2;
-      return 1.0f / (s2 * sqrtf(1.0f + t * t));
-    }
-    // (sigma^2 + x^2)^(a-1) as exp2((a-1) log2(.)): the base is a normal
-    // positive float (sigma^2 + x^2 >= sigma^2), so the hardware v_log_f32 /
-    // v_exp_f32 pair (~1 ulp each) replaces the ~30-instruction general powf
-    case OF_PEN_GEN_CHARBONNIER:
-      return 2.0f * p.p1 * __builtin_amdgcn_exp2f((p.p1 - 1.0f) * __builtin_amdgcn_logf(p.p0 * p.p0 + x * x));
+    case OF_PEN_QUADRATIC: return pen_quad(p, x);
+    case OF_PEN_LORENTZIAN: return pen_lorentz(p, x);
+    case OF_PEN_CHARBONNIER: return pen_charb(p, x);
+    case OF_PEN_GEN_CHARBONNIER: return pen_gcharb(p, x);
     case OF_PEN_GEMAN_MCCLURE: {
       float s2 = p.p0 * p.p0, d = s2 + x * x;
       return 2.0f * s2 / (d * d);
@@ -83,6 +91,15 @@ __device__ __forceinline__ float pen_w(const PenF &p, float x) {
     case OF_PEN_TDIST_UNNORM: return (p.p0 + 1.0f) / (p.p1 * p.p1 * p.p0 + x * x);
     default: return p.p0;  // OF_PEN_CONST
   }
+}
+template <int K>
+__device__ __forceinline__ float pen_k(const PenF &p, float x) {
+  if constexpr (K == OF_PEN_QUADRATIC) return pen_quad(p, x);
+  else if constexpr (K == OF_PEN_LORENTZIAN) return pen_lorentz(p, x);
+  else if constexpr (K == OF_PEN_CHARBONNIER) return pen_charb(p, x);
+  else if constexpr (K == OF_PEN_GEN_CHARBONNIER) return pen_gcharb(p, x);
+  else if constexpr (K == OF_PEN_CONST) return p.p0;
+  else return pen_w(p, x);
 }
 
 // rho'(x)/x in fp64 (penalties.py d_type == 2, the reference's own float64

@@ -205,6 +205,9 @@ static void create_stream(hipStream_t *s) {
   HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
 }
 
+#ifndef OF_FUSED_WARP_DEFAULT
+#define OF_FUSED_WARP_DEFAULT 1
+#endif
 struct of_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -247,6 +250,7 @@ struct of_ctx {
   std::chrono::steady_clock::time_point prog_t0;
   std::vector<float> prog_uv;  // host copy of a stage's flow (OF_PROGRESS_FLOW)
   int opt_sor_pipe = 1;    // of_set_option(OF_OPT_SOR_PIPELINE)
+  int opt_fused_warp = OF_FUSED_WARP_DEFAULT;  // of_set_option(OF_OPT_FUSED_WARP)
   // solve log (of_set_solve_log): fp64 true residual of every solve
   int slog = 0;
   struct SolveLog {
@@ -648,12 +652,76 @@ OpArgs op_args(const of_params *P, double alpha, double lambda2) {
   return o;
 }
 
+// the assembly kernels' penalty mode (kernels_flow.hip, PenMode): the
+// quadratic stage or a robust stage whose penalties share one kind get a
+// specialised kernel, anything else the run-time form
+int pen_mode(const OpArgs &o) {
+  auto all = [](std::initializer_list<const PenF *> ps, int kind) {
+    for (const PenF *p : ps)
+      if (p->kind != kind) return false;
+    return true;
+  };
+  if (o.use_q && !o.use_r)
+    return all({&o.qd, &o.qsu[0], &o.qsu[1], &o.qsv[0], &o.qsv[1]}, OF_PEN_QUADRATIC) ? OF_PM_Q : OF_PM_ANY;
+  if (o.use_r && !o.use_q) {
+    const int k = o.rd.kind;
+    if ((k == OF_PEN_GEN_CHARBONNIER || k == OF_PEN_CHARBONNIER || k == OF_PEN_LORENTZIAN || k == OF_PEN_CONST) &&
+        all({&o.rsu[0], &o.rsu[1], &o.rsv[0], &o.rsv[1]}, k))
+      return OF_PM_R(k);
+  }
+  return OF_PM_ANY;
+}
+// calls f(kernel) with the instantiation of template K for mode m
+#define OF_BY_PM(m, KT, ...)                                                               \
+  switch (m) {                                                                            \
+    case OF_PM_Q: f(KT<__VA_ARGS__ OF_PM_Q>); break;                                      \
+    case OF_PM_R(OF_PEN_GEN_CHARBONNIER): f(KT<__VA_ARGS__ OF_PM_R(OF_PEN_GEN_CHARBONNIER)>); break; \
+    case OF_PM_R(OF_PEN_CHARBONNIER): f(KT<__VA_ARGS__ OF_PM_R(OF_PEN_CHARBONNIER)>); break; \
+    case OF_PM_R(OF_PEN_LORENTZIAN): f(KT<__VA_ARGS__ OF_PM_R(OF_PEN_LORENTZIAN)>); break; \
+    case OF_PM_R(OF_PEN_CONST): f(KT<__VA_ARGS__ OF_PM_R(OF_PEN_CONST)>); break;           \
+    default: f(KT<__VA_ARGS__ OF_PM_ANY>); break;                                          \
+  }
+
 void flow_operator(of_ctx *c, const OpArgs &o, const F2 &uv, const F2 *duv, const Img &It, const Img &Ix,
                    const Img &Iy, const F2 *uvhat, const Img &coef, const F2 &rhs) {
   Grid2 g = grid2(uv.H, uv.W);
-  launch(c, "flow_operator", o.f64 ? k_flow_operator_f64 : k_flow_operator, g.grid, g.block, 0, o, (const float2 *)uv.p,
-         (const float2 *)(duv ? duv->p : nullptr), (const float *)It.p, (const float *)Ix.p, (const float *)Iy.p, It.C,
-         (const float2 *)(uvhat ? uvhat->p : nullptr), uv.H, uv.W, uv.P, coef.ps(), coef.p, rhs.p);
+  auto f = [&](auto kern) {
+    launch(c, "flow_operator", kern, g.grid, g.block, 0, o, (const float2 *)uv.p,
+           (const float2 *)(duv ? duv->p : nullptr), (const float *)It.p, (const float *)Ix.p, (const float *)Iy.p,
+           It.C, (const float2 *)(uvhat ? uvhat->p : nullptr), uv.H, uv.W, uv.P, coef.ps(), coef.p, rhs.p);
+  };
+  if (o.f64) {
+    f(k_flow_operator_f64);
+    return;
+  }
+  const int m = uvhat ? OF_PM_ANY : pen_mode(o);
+  OF_BY_PM(m, k_flow_operator, )
+}
+
+// partial_deriv + flow_operator fused (k_warp_operator): no It / Ix / Iy
+// planes; nc = 1 or 3 image channels, the fp32 assembly, no duv / uvhat
+bool can_fuse_warp_op(const of_ctx *c, const OpArgs &o, int nc) {
+  return c->opt_fused_warp && !o.f64 && (nc == 1 || nc == 3);
+}
+void warp_operator(of_ctx *c, const LevelDeriv &L, int interp, const OpArgs &o, const F2 &uv, const Img &coef,
+                   const F2 &rhs) {
+  Grid2 g = grid2(uv.H, uv.W);
+  const size_t ps = coef.ps();
+  REQUIRE(L.I1x.ps() == ps && L.args.nc == L.I1x.C, OF_EHIP, "warp_operator: plane strides differ");
+  const float2 *u = (const float2 *)uv.p;
+  const char *name = interp == OF_INTERP_BICUBIC ? "warp_operator_hermite"
+                     : interp == OF_INTERP_CUBIC ? "warp_operator_bspline"
+                                                 : "warp_operator_bilinear";
+  auto f = [&](auto kern) { launch(c, name, kern, g.grid, g.block, 0, L.args, o, u, uv.H, uv.W, uv.P, ps, coef.p, rhs.p); };
+  const int m = pen_mode(o);
+  const bool one = L.args.nc == 1;
+  if (interp == OF_INTERP_BICUBIC) {
+    if (one) { OF_BY_PM(m, k_warp_operator, 1, 1, ) } else { OF_BY_PM(m, k_warp_operator, 1, 3, ) }
+  } else if (interp == OF_INTERP_CUBIC) {
+    if (one) { OF_BY_PM(m, k_warp_operator, 0, 1, ) } else { OF_BY_PM(m, k_warp_operator, 0, 3, ) }
+  } else {
+    if (one) { OF_BY_PM(m, k_warp_operator, 2, 1, ) } else { OF_BY_PM(m, k_warp_operator, 2, 3, ) }
+  }
 }
 
 // ---- iterative solve (base.py:87-172) -----------------------------------------
@@ -1567,9 +1635,14 @@ void hs_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, of_stats *
   F2 rhs = new_f2(c, H, W), x = new_f2(c, H, W), tmp = new_f2(c, H, W);
   OpArgs o = op_args(P, 0.0, 0.0);
   Grid2 g = grid2(H, W);
+  const bool fuse = can_fuse_warp_op(c, o, nc);
   for (int it = 0; it < P->max_warping_iters; ++it) {
-    partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
-    flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
+    if (fuse) {
+      warp_operator(c, D, P->interp, o, uv, coef, rhs);
+    } else {
+      partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
+      flow_operator(c, o, uv, nullptr, It, Ix, Iy, nullptr, coef, rhs);
+    }
     note_solve(c, st, solve_tok(c, P, coef, rhs, x));
     c->cur_px = (double)H * W;
     const double xn = std::sqrt(norm2(c, x));
@@ -1608,12 +1681,17 @@ void irls_base(of_ctx *c, const of_params *P, const LevelIn &L, F2 &uv, double a
   const bool gen = P->filters.general;
   GenLevel GL;
   if (gen) GL = gen_level(c, P, H, W);
+  // one linearisation per warp: warp + assembly fused (no derivative planes)
+  const bool fuse = !gen && max_linear == 1 && can_fuse_warp_op(c, o, nc);
   for (int it = 0; it < P->max_iters; ++it) {
-    partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
+    if (!fuse) partial_deriv(c, D, P->interp, uv, It, Ix, Iy);
     for (int jl = 0; jl < max_linear; ++jl) {
       if (gen) {
         gen_flow_operator(c, P, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, GL, rhs);
         note_solve(c, st, gen_solve_logged(c, P, GL, rhs, x));
+      } else if (fuse) {
+        warp_operator(c, D, P->interp, o, uv, coef, rhs);
+        note_solve(c, st, solve_tok(c, P, coef, rhs, x));
       } else {
         flow_operator(c, o, uv, jl ? &duv : nullptr, It, Ix, Iy, nullptr, coef, rhs);
         note_solve(c, st, solve_tok(c, P, coef, rhs, x));
@@ -2058,6 +2136,9 @@ int of_set_option(of_ctx *c, int option, int value) {
     case OF_OPT_SOR_PIPELINE:
       c->opt_sor_pipe = value ? 1 : 0;
       return OF_OK;
+    case OF_OPT_FUSED_WARP:
+      c->opt_fused_warp = value ? 1 : 0;
+      return OF_OK;
     default:
       c->err = "unknown option";
       return OF_EINVAL;
@@ -2077,6 +2158,9 @@ int of_get_option(of_ctx *c, int option, int64_t *value) {
   switch (option) {
     case OF_OPT_SOR_PIPELINE:
       *value = c->opt_sor_pipe;
+      return OF_OK;
+    case OF_OPT_FUSED_WARP:
+      *value = c->opt_fused_warp;
       return OF_OK;
     case OF_OPT_SOR_FALLBACKS: {
       int64_t n = c->sor_fallbacks;
@@ -2364,6 +2448,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
       l->opt_sor_pipe = c->opt_sor_pipe;
+      l->opt_fused_warp = c->opt_fused_warp;
       if (l != c) l->epoch = c->epoch;
       l->big = big_px > 0 ? &c->big_own : nullptr;
       l->big_px = big_px;
@@ -2597,6 +2682,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
       of_ctx *l = li ? c->lanes[li - 1] : c;
       l->prof = c->prof;
       l->opt_sor_pipe = c->opt_sor_pipe;
+      l->opt_fused_warp = c->opt_fused_warp;
       if (l != c) l->epoch = c->epoch;
       l->big = OF_BIG_PX > 0 ? &c->big_own : nullptr;
       l->big_px = OF_BIG_PX;
@@ -2794,6 +2880,7 @@ int of_pairs_open(of_ctx *c, int H, int W, int C, const of_params *P, int lanes)
       pp->lanes.push_back(l);
       l->prof = 0;
       l->opt_sor_pipe = c->opt_sor_pipe;
+      l->opt_fused_warp = c->opt_fused_warp;
       l->big = lanes > 1 && OF_BIG_PX > 0 ? &c->big_own : nullptr;
       l->big_px = OF_BIG_PX;
       stage_alloc(l, c, 2 * (size_t)H * W * C, nu);

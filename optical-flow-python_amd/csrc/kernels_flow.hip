@@ -30,14 +30,34 @@ __device__ __forceinline__ float bspline3(float t) {
 }
 
 // partial_deriv (derivatives.py:148-296) for one pixel and all channels.
-// (x2, y2) are the 1-based warped coordinates.
-// writes It, Ix, Iy of every channel straight to the output planes (no
-// per-channel register arrays: a runtime-indexed array would live in scratch)
-template <int INTERP>
+// (x2, y2) are the 1-based warped coordinates.  Each channel's (It, Ix, Iy)
+// goes to out(c, it, ix, iy): PlaneOut stores it straight to the planes (no
+// per-channel register arrays: a runtime-indexed array would live in
+// scratch); RegOut<NC> keeps it in registers for the fused warp + assembly
+// (NC > 0: the channel loop is unrolled, so the array index is static).
+struct PlaneOut {
+  float *It, *Ix, *Iy;
+  size_t ps, k;
+  __device__ __forceinline__ void operator()(int c, float it, float ix, float iy) const {
+    It[c * ps + k] = it;
+    Ix[c * ps + k] = ix;
+    Iy[c * ps + k] = iy;
+  }
+};
+template <int NC>
+struct RegOut {
+  float it[NC], ix[NC], iy[NC];
+  __device__ __forceinline__ void operator()(int c, float a, float b, float e) {
+    it[c] = a;
+    ix[c] = b;
+    iy[c] = e;
+  }
+};
+template <int INTERP, int NC, typename Out>
 __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int P, size_t ps, int i, int j, float x2,
-                                           float y2, float *__restrict__ It, float *__restrict__ Ix,
-                                           float *__restrict__ Iy) {
+                                           float y2, Out &out) {
   const size_t k = (size_t)i * P + j;
+  const int nc = NC > 0 ? NC : d.nc;
   if (INTERP == OF_INTERP_BICUBIC) {
     float fx = floorf(x2), fy = floorf(y2);
     bool oob = (fx < 1.0f) || (fx + 1.0f > (float)W) || (fy < 1.0f) || (fy + 1.0f > (float)H) || !(x2 == x2) ||
@@ -49,7 +69,8 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
     hermite(ax, hx, dhx);
     hermite(ay, hy, dhy);
     const size_t cs[4] = {(size_t)fy0 * P + fx0, (size_t)fy0 * P + cx0, (size_t)cy0 * P + fx0, (size_t)cy0 * P + cx0};
-    for (int c = 0; c < d.nc; ++c) {
+#pragma unroll
+    for (int c = 0; c < nc; ++c) {
       const size_t o = c * ps;
       float v = 0.0f, vx = 0.0f, vy = 0.0f;
 #pragma unroll
@@ -61,18 +82,16 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
         vx += dhx[xi] * gy * z + dhx[2 + xi] * gy * dx + dhx[xi] * sy * dy + dhx[2 + xi] * sy * dxy;
         vy += gx * dhy[yi] * z + sx * dhy[yi] * dx + gx * dhy[2 + yi] * dy + sx * dhy[2 + yi] * dxy;
       }
-      if (oob) {
-        It[o + k] = Ix[o + k] = Iy[o + k] = 0.0f;
-      } else {
-        It[o + k] = v - d.I1[o + k];
-        Ix[o + k] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
-        Iy[o + k] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
-      }
+      if (oob) out(c, 0.0f, 0.0f, 0.0f);
+      else
+        out(c, v - d.I1[o + k], d.blend * vx + (1.0f - d.blend) * d.I1x[o + k],
+            d.blend * vy + (1.0f - d.blend) * d.I1y[o + k]);
     }
   } else {
-    const bool out = (x2 > (float)W) || (x2 < 1.0f) || (y2 > (float)H) || (y2 < 1.0f) || !(x2 == x2) || !(y2 == y2);
-    if (out) {
-      for (int c = 0; c < d.nc; ++c) It[c * ps + k] = Ix[c * ps + k] = Iy[c * ps + k] = 0.0f;
+    const bool outside = (x2 > (float)W) || (x2 < 1.0f) || (y2 > (float)H) || (y2 < 1.0f) || !(x2 == x2) || !(y2 == y2);
+    if (outside) {
+#pragma unroll
+      for (int c = 0; c < nc; ++c) out(c, 0.0f, 0.0f, 0.0f);
       return;
     }
     const float r = y2 - 1.0f, q = x2 - 1.0f;
@@ -87,7 +106,8 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
         rr[a] = ext_mirror(i0 + a - 1, H);
         cc[a] = ext_mirror(j0 + a - 1, W);
       }
-      for (int c = 0; c < d.nc; ++c) {
+#pragma unroll
+      for (int c = 0; c < nc; ++c) {
         const size_t o = c * ps;
         float v = 0.0f, vx = 0.0f, vy = 0.0f;
 #pragma unroll
@@ -104,23 +124,22 @@ __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int
           vx += wr[a] * tx;
           vy += wr[a] * ty;
         }
-        It[o + k] = v - d.I1[o + k];
-        Ix[o + k] = d.blend * vx + (1.0f - d.blend) * d.I1x[o + k];
-        Iy[o + k] = d.blend * vy + (1.0f - d.blend) * d.I1y[o + k];
+        out(c, v - d.I1[o + k], d.blend * vx + (1.0f - d.blend) * d.I1x[o + k],
+            d.blend * vy + (1.0f - d.blend) * d.I1y[o + k]);
       }
     } else {  // bi-linear
       int i0 = (int)floorf(r), j0 = (int)floorf(q);
       float fr = r - i0, fc = q - j0;
       int i1 = min(i0 + 1, H - 1), j1 = min(j0 + 1, W - 1);
-      for (int c = 0; c < d.nc; ++c) {
+#pragma unroll
+      for (int c = 0; c < nc; ++c) {
         const size_t o = c * ps;
         auto bil = [&](const float *p) {
           const float *r0 = p + o + (size_t)i0 * P, *r1 = p + o + (size_t)i1 * P;
           return (1.0f - fr) * ((1.0f - fc) * r0[j0] + fc * r0[j1]) + fr * ((1.0f - fc) * r1[j0] + fc * r1[j1]);
         };
-        It[o + k] = bil(d.I2) - d.I1[o + k];
-        Ix[o + k] = d.blend * bil(d.A) + (1.0f - d.blend) * d.I1x[o + k];
-        Iy[o + k] = d.blend * bil(d.B) + (1.0f - d.blend) * d.I1y[o + k];
+        out(c, bil(d.I2) - d.I1[o + k], d.blend * bil(d.A) + (1.0f - d.blend) * d.I1x[o + k],
+            d.blend * bil(d.B) + (1.0f - d.blend) * d.I1y[o + k]);
       }
     }
   }
@@ -137,7 +156,8 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_partial_deriv(DerivArgs d, con
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     float2 f = uv[k];
-    warp_pixel<INTERP>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, It, Ix, Iy);
+    PlaneOut out{It, Ix, Iy, ps, k};
+    warp_pixel<INTERP, 0>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, out);
   }
 }
 template __global__ void k_partial_deriv<0>(DerivArgs, const float2 *, int, int, int, size_t, float *, float *, float *);
@@ -146,10 +166,29 @@ template __global__ void k_partial_deriv<2>(DerivArgs, const float2 *, int, int,
 
 // ---------------------------------------------------------------------------
 // matrix-free flow operator
+// Penalty mode of an assembly kernel: OF_PM_ANY decides everything at run
+// time (use_q / use_r, each penalty's kind); otherwise the system is the
+// quadratic relaxation only (OF_PM_Q, alpha == 1, every penalty quadratic) or
+// the robust one only (OF_PM_R(kind), alpha == 0, every robust penalty of
+// that kind).  The arithmetic is the generic form's, term for term.
+#define OF_PM_ANY (-1)
+#define OF_PM_Q 0
+#define OF_PM_R(kind) (1 + (kind))
+template <int M>
+struct PenMode {
+  static constexpr bool any = M == OF_PM_ANY;
+  static constexpr int kind = M == OF_PM_ANY ? -1 : M == OF_PM_Q ? OF_PEN_QUADRATIC : M - 1;
+  __device__ static bool q(const OpArgs &o) { return any ? o.use_q : M == OF_PM_Q; }
+  __device__ static bool r(const OpArgs &o) { return any ? o.use_r : M != OF_PM_Q; }
+  __device__ static float pen(const PenF &p, float x) { return pen_k<kind>(p, x); }
+};
+
+template <int M = OF_PM_ANY>
 __device__ __forceinline__ float2 edge_w(const OpArgs &o, int axis, float du, float dv) {
+  using PM = PenMode<M>;
   float wu = 0.0f, wv = 0.0f;
-  if (o.use_q) { wu += o.aq_s * pen_w(o.qsu[axis], du); wv += o.aq_s * pen_w(o.qsv[axis], dv); }
-  if (o.use_r) { wu += o.ar_s * pen_w(o.rsu[axis], du); wv += o.ar_s * pen_w(o.rsv[axis], dv); }
+  if (PM::q(o)) { wu += o.aq_s * PM::pen(o.qsu[axis], du); wv += o.aq_s * PM::pen(o.qsv[axis], dv); }
+  if (PM::r(o)) { wu += o.ar_s * PM::pen(o.rsu[axis], du); wv += o.ar_s * PM::pen(o.rsv[axis], dv); }
   return make_float2(wu, wv);
 }
 
@@ -159,7 +198,69 @@ __device__ __forceinline__ float2 ld_uvd(const float2 *uv, const float2 *duv, si
   return a;
 }
 
-// coef planes: 0 wx_u, 1 wy_u, 2 wx_v, 3 wy_v, 4 a_uu, 5 a_uv, 6 a_vv; rhs float2
+// coef planes: 0 wx_u, 1 wy_u, 2 wx_v, 3 wy_v, 4 a_uu, 5 a_uv, 6 a_vv; rhs float2.
+// One pixel's row of the system; deriv(ch, It, Ix, Iy) fetches channel ch's
+// derivatives (planes, or the fused kernel's registers).
+template <int NC, int M, typename Deriv>
+__device__ __forceinline__ void assemble_px(const OpArgs &o, const float2 *__restrict__ uv,
+                                            const float2 *__restrict__ duv, int nc_rt, const float2 *__restrict__ uvhat,
+                                            int i, int j, int H, int W, int P, size_t ps, float *__restrict__ coef,
+                                            float2 *__restrict__ rhs, const Deriv &deriv) {
+  using PM = PenMode<M>;
+  const int nc = NC > 0 ? NC : nc_rt;
+  const size_t k = (size_t)i * P + j;
+  const float2 c = ld_uvd(uv, duv, k);
+  float2 eR = make_float2(0.f, 0.f), eD = eR, eL = eR, eU = eR;
+  if (j < W - 1) { float2 n = ld_uvd(uv, duv, k + 1); eR = edge_w<M>(o, 0, n.x - c.x, n.y - c.y); }
+  if (i < H - 1) { float2 n = ld_uvd(uv, duv, k + P); eD = edge_w<M>(o, 1, n.x - c.x, n.y - c.y); }
+  if (j > 0) { float2 n = ld_uvd(uv, duv, k - 1); eL = edge_w<M>(o, 0, c.x - n.x, c.y - n.y); }
+  if (i > 0) { float2 n = ld_uvd(uv, duv, k - P); eU = edge_w<M>(o, 1, c.x - n.x, c.y - n.y); }
+  // data term, channel-averaged (classic_nl.py:330-343)
+  float du = 0.f, dv = 0.f;
+  if (duv) { du = duv[k].x; dv = duv[k].y; }
+  float psq = 0.f, psr = 0.f, ix2 = 0.f, iy2 = 0.f, ixy = 0.f, itx = 0.f, ity = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < nc; ++ch) {
+    float it, gx, gy;
+    deriv(ch, it, gx, gy);
+    const float itl = it + gx * du + gy * dv;
+    if (PM::q(o)) psq += PM::pen(o.qd, itl);
+    if (PM::r(o)) psr += PM::pen(o.rd, itl);
+    ix2 += gx * gx; iy2 += gy * gy; ixy += gx * gy;
+    itx += itl * gx; ity += itl * gy;
+  }
+  const float inv = 1.0f / (float)nc;
+  const float psi = ((PM::q(o) ? o.aq_d * psq : 0.f) + (PM::r(o) ? o.ar_d * psr : 0.f)) * inv;
+  ix2 *= inv; iy2 *= inv; ixy *= inv; itx *= inv; ity *= inv;
+  // b uses uv (not uv + duv): classic_nl.py:362-367
+  const float2 u0 = uv[k];
+  float lu = 0.f, lv = 0.f;
+  if (j < W - 1) { float2 n = uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
+  if (i < H - 1) { float2 n = uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
+  if (j > 0) { float2 n = uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
+  if (i > 0) { float2 n = uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
+  float auu = psi * ix2 + (eL.x + eR.x + eU.x + eD.x);
+  float avv = psi * iy2 + (eL.y + eR.y + eU.y + eD.y);
+  float bu = -lu - psi * itx, bv = -lv - psi * ity;
+  if (uvhat) {  // AltBA coupling (alt_ba.py:236-242)
+    const float2 h = uvhat[k];
+    const float tu = pen_w(o.rc, u0.x - h.x), tv = pen_w(o.rc, u0.y - h.y);
+    auu += o.lambda2 * tu;
+    avv += o.lambda2 * tv;
+    bu += o.lambda2 * tu * (h.x - u0.x);
+    bv += o.lambda2 * tv * (h.y - u0.y);
+  }
+  coef[k] = eR.x;
+  coef[ps + k] = eD.x;
+  coef[2 * ps + k] = eR.y;
+  coef[3 * ps + k] = eD.y;
+  coef[4 * ps + k] = auu;
+  coef[5 * ps + k] = psi * ixy;
+  coef[6 * ps + k] = avv;
+  rhs[k] = make_float2(bu, bv);
+}
+
+template <int M>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const float2 *__restrict__ uv, const float2 *__restrict__ duv,
                                 const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
                                 int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
@@ -167,55 +268,53 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
   OF_FOR_PIXELS(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
-    const float2 c = ld_uvd(uv, duv, k);
-    float2 eR = make_float2(0.f, 0.f), eD = eR, eL = eR, eU = eR;
-    if (j < W - 1) { float2 n = ld_uvd(uv, duv, k + 1); eR = edge_w(o, 0, n.x - c.x, n.y - c.y); }
-    if (i < H - 1) { float2 n = ld_uvd(uv, duv, k + P); eD = edge_w(o, 1, n.x - c.x, n.y - c.y); }
-    if (j > 0) { float2 n = ld_uvd(uv, duv, k - 1); eL = edge_w(o, 0, c.x - n.x, c.y - n.y); }
-    if (i > 0) { float2 n = ld_uvd(uv, duv, k - P); eU = edge_w(o, 1, c.x - n.x, c.y - n.y); }
-    // data term, channel-averaged (classic_nl.py:330-343)
-    float du = 0.f, dv = 0.f;
-    if (duv) { du = duv[k].x; dv = duv[k].y; }
-    float psq = 0.f, psr = 0.f, ix2 = 0.f, iy2 = 0.f, ixy = 0.f, itx = 0.f, ity = 0.f;
-    for (int ch = 0; ch < nc; ++ch) {
+    assemble_px<0, M>(o, uv, duv, nc, uvhat, i, j, H, W, P, ps, coef, rhs, [&](int ch, float &it, float &gx, float &gy) {
       const size_t kc = ch * ps + k;
-      const float gx = Ix[kc], gy = Iy[kc], itl = It[kc] + gx * du + gy * dv;
-      if (o.use_q) psq += pen_w(o.qd, itl);
-      if (o.use_r) psr += pen_w(o.rd, itl);
-      ix2 += gx * gx; iy2 += gy * gy; ixy += gx * gy;
-      itx += itl * gx; ity += itl * gy;
-    }
-    const float inv = 1.0f / (float)nc;
-    const float psi = ((o.use_q ? o.aq_d * psq : 0.f) + (o.use_r ? o.ar_d * psr : 0.f)) * inv;
-    ix2 *= inv; iy2 *= inv; ixy *= inv; itx *= inv; ity *= inv;
-    // b uses uv (not uv + duv): classic_nl.py:362-367
-    const float2 u0 = uv[k];
-    float lu = 0.f, lv = 0.f;
-    if (j < W - 1) { float2 n = uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
-    if (i < H - 1) { float2 n = uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
-    if (j > 0) { float2 n = uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
-    if (i > 0) { float2 n = uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
-    float auu = psi * ix2 + (eL.x + eR.x + eU.x + eD.x);
-    float avv = psi * iy2 + (eL.y + eR.y + eU.y + eD.y);
-    float bu = -lu - psi * itx, bv = -lv - psi * ity;
-    if (uvhat) {  // AltBA coupling (alt_ba.py:236-242)
-      const float2 h = uvhat[k];
-      const float tu = pen_w(o.rc, u0.x - h.x), tv = pen_w(o.rc, u0.y - h.y);
-      auu += o.lambda2 * tu;
-      avv += o.lambda2 * tv;
-      bu += o.lambda2 * tu * (h.x - u0.x);
-      bv += o.lambda2 * tv * (h.y - u0.y);
-    }
-    coef[k] = eR.x;
-    coef[ps + k] = eD.x;
-    coef[2 * ps + k] = eR.y;
-    coef[3 * ps + k] = eD.y;
-    coef[4 * ps + k] = auu;
-    coef[5 * ps + k] = psi * ixy;
-    coef[6 * ps + k] = avv;
-    rhs[k] = make_float2(bu, bv);
+      it = It[kc];
+      gx = Ix[kc];
+      gy = Iy[kc];
+    });
   }
 }
+
+// Warp + derivatives + assembly in one pass: the
+// per-channel It / Ix / Iy of a pixel stay in registers, so the 24 B/px
+// round trip of the three planes (nc = 1) and one launch per warping
+// iteration go away.  Same arithmetic as k_partial_deriv + k_flow_operator.
+template <int INTERP, int NC, int M>
+__global__ __launch_bounds__(OF_BX *OF_BY) void k_warp_operator(DerivArgs d, OpArgs o, const float2 *__restrict__ uv,
+                                                                int H, int W, int P, size_t ps,
+                                                                float *__restrict__ coef, float2 *__restrict__ rhs) {
+  OF_FOR_PIXELS(H, W) {
+    if (j >= W) continue;
+    const size_t k = (size_t)i * P + j;
+    const float2 f = uv[k];
+    RegOut<NC> r;
+    warp_pixel<INTERP, NC>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, r);
+    assemble_px<NC, M>(o, uv, (const float2 *)nullptr, NC, (const float2 *)nullptr, i, j, H, W, P, ps, coef, rhs,
+                    [&](int ch, float &it, float &gx, float &gy) {
+                      it = r.it[ch];
+                      gx = r.ix[ch];
+                      gy = r.iy[ch];
+                    });
+  }
+}
+#define OF_WOP(I, N, M) template __global__ void k_warp_operator<I, N, M>(DerivArgs, OpArgs, const float2 *, int, int, \
+                                                                          int, size_t, float *, float2 *);
+#define OF_FOP(M) template __global__ void k_flow_operator<M>(OpArgs, const float2 *, const float2 *, const float *, \
+                                                              const float *, const float *, int, const float2 *, int, \
+                                                              int, int, size_t, float *, float2 *);
+// specialised penalty modes: the registry's quadratic stage and its robust
+// stages (generalized Charbonnier: Classic+NL; Charbonnier: Classic-C;
+// Lorentzian: BA; Horn-Schunck's constant weights)
+#define OF_PM_LIST(X) X(OF_PM_ANY) X(OF_PM_Q) X(OF_PM_R(OF_PEN_GEN_CHARBONNIER)) X(OF_PM_R(OF_PEN_CHARBONNIER)) \
+  X(OF_PM_R(OF_PEN_LORENTZIAN)) X(OF_PM_R(OF_PEN_CONST))
+#define OF_WOP_M(M) OF_WOP(0, 1, M) OF_WOP(1, 1, M) OF_WOP(2, 1, M) OF_WOP(0, 3, M) OF_WOP(1, 3, M) OF_WOP(2, 3, M)
+OF_PM_LIST(OF_WOP_M)
+OF_PM_LIST(OF_FOP)
+#undef OF_WOP_M
+#undef OF_WOP
+#undef OF_FOP
 
 // The same assembly with every intermediate in fp64 (the reference's own
 // precision) and one rounding per stored plane: for AltBA (OpArgs::f64),
