@@ -180,31 +180,21 @@ struct HostStage {
 #define OF_SORP_SYNC_BYTES (1024 + SOR_RING_MAX * 2 * SOR_MAXS * sizeof(int))
 #define OF_SORP_BYTES (OF_SORP_SYNC_BYTES + (SOR_RING_MAX * 2 * SOR_MAXS * 2 + SOR_RING_MAX * 2) * sizeof(double))
 
-// Streams: OF_STREAM_QUEUE=shared (env, A/B) creates plain non-blocking
-// streams, which the runtime maps onto its GPU_MAX_HW_QUEUES (4) hardware
-// queues by creation order -- after other contexts' streams came and went,
-// two busy batch lanes can land on one queue and serialise (measured: 8
-// 1080p pairs x 4 lanes, 45.7 pairs/s on a fresh context, 42.0 after a pair
-// pool's lanes were destroyed on it; tools/order_probe.py).  The default
-// gives every stream a queue of its own: a stream with a CU mask (here all
-// CUs) always gets a dedicated hardware queue.
-static void create_stream(hipStream_t *s) {
-  static const bool shared = [] {
-    const char *e = getenv("OF_STREAM_QUEUE");
-    return e && !strcmp(e, "shared");
-  }();
-  if (!shared) {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0xffffffffu);
-      if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
-      if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return;
-    }
-  }
-  HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-}
+// Streams are plain non-blocking streams, which the runtime maps onto its
+// GPU_MAX_HW_QUEUES (4 on the box) hardware queues by creation order: batch
+// lanes created after other streams of the same process came and went can
+// share a queue with a busy lane and serialise (8 1080p pairs x 4 lanes:
+// 47.0 pairs/s with a context's lanes created first, 43.1 with them created
+// after a pair pool's lanes were destroyed on that context;
+// tools/order_probe.py, profiles/r5_order_probe.log).  Streams created with a
+// full CU mask behaved the same (the runtime pools them too).  Keep long-lived
+// lanes: a context creates its of_pairs_run lanes once and keeps them.
+static void create_stream(hipStream_t *s) { HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking)); }
 
+// batch lanes created together on first use (ensure_lanes): the default 4
+#ifndef OF_LANES_MIN
+#define OF_LANES_MIN 4
+#endif
 #ifndef OF_FUSED_WARP_DEFAULT
 #define OF_FUSED_WARP_DEFAULT 1
 #endif
@@ -2145,9 +2135,11 @@ int of_set_option(of_ctx *c, int option, int value) {
   }
 }
 
+void pool_set_progress(PairPool *pp, of_progress_fn fn);
 int of_set_progress(of_ctx *c, of_progress_fn fn, void *user, int flags) {
   if (!c) return OF_EINVAL;
-  c->prog_fn = fn;
+  if (c->pool) pool_set_progress(c->pool, fn);  // takes effect when the pair stream closes
+  else c->prog_fn = fn;
   c->prog_user = user;
   c->prog_flags = flags;
   return OF_OK;
@@ -2410,6 +2402,45 @@ int of_pair_run(of_ctx *c, int slot, of_params *P, of_stats *st) {
 // another pair's kernels fill the CUs.  Every kernel is deterministic, so a
 // slot's flow does not depend on the lane count.  lanes == 1 runs the slots
 // in order on the ctx's own stream.
+namespace {
+// The batch lanes (of_pairs_run, of_pairs_run_host, the pair pool) are the
+// context itself (lane 0) and its child contexts (lanes 1..), created once,
+// in one consecutive batch, and kept.  The runtime binds each stream to one of
+// its GPU_MAX_HW_QUEUES (4) hardware queues when the stream is created: the
+// first four streams of a process get four queues, later ones share them, so
+// two busy lanes can end up on one queue and serialise (43 vs 47 pairs/s).
+// rocprofv3's Queue_Id per lane thread (tools/queue_map.py,
+// profiles/r5_queue_map_*.txt) showed it: lanes created and destroyed per
+// pool, or a fifth lane stream, collided; the context's stream plus three
+// children created right after it did not.  n = child lanes wanted.
+void ensure_lanes(of_ctx *c, int n) {
+  const int want = std::max(n, OF_LANES_MIN - 1);
+  while ((int)c->lanes.size() < want) {
+    of_ctx *l = nullptr;
+    const int rc = of_ctx_create(c->device, &l);
+    REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
+    c->lanes.push_back(l);
+  }
+}
+// profiling: the child lanes' timings into the ctx's table (lane 0, the ctx,
+// records its own)
+void merge_lane_prof(of_ctx *c, int lanes) {
+  c->big = nullptr;
+  for (int li = 1; li < lanes; ++li) {
+    of_ctx *l = c->lanes[li - 1];
+    for (auto &kv : l->ktimes) {
+      KTime &d = c->ktimes[kv.first];
+      d.ms += kv.second.ms;
+      d.px += kv.second.px;
+      d.n += kv.second.n;
+    }
+    l->ktimes.clear();
+    c->tl.insert(c->tl.end(), l->tl.begin(), l->tl.end());
+    l->tl.clear();
+  }
+}
+}  // namespace
+
 int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats *st) {
   API_BEGIN(c)
   REQUIRE(P && nslots >= 1 && nslots <= (int)c->slots.size() && lanes >= 1 && lanes <= 16, OF_EINVAL,
@@ -2428,16 +2459,8 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       run_slot(c, c->slots[s], &Pc, s == 0 ? st : nullptr);
     }
   } else {
-    // lane 0 is the ctx itself (its stream), lanes 1.. are child contexts:
-    // `lanes` streams in all, within GPU_MAX_HW_QUEUES (4) for lanes <= 4
-    // (of_pairs_run_host adds its copy stream, see HostStage)
-    while ((int)c->lanes.size() < lanes - 1) {
-      of_ctx *l = nullptr;
-      const int rc = of_ctx_create(c->device, &l);
-      REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
-      c->lanes.push_back(l);
-
-    }
+    // lane 0 is the ctx itself, lanes 1.. its long-lived children (ensure_lanes)
+    ensure_lanes(c, lanes - 1);
     // big-phase token threshold in pixels.  8 1080p pairs, 2 lanes: 22.5
     // pairs/s with the token in three runs (16-18 without; 20.5 with one
     // lane) -- two lanes' fine-level CG kernels otherwise stall each other
@@ -2473,18 +2496,7 @@ int of_pairs_run(of_ctx *c, int nslots, const of_params *P, int lanes, of_stats 
       });
     }
     for (auto &t : th) t.join();
-    c->big = nullptr;
-    for (int li = 1; li < lanes; ++li) {  // profiling: lane timings into the ctx's table
-      for (auto &kv : c->lanes[li - 1]->ktimes) {
-        KTime &d = c->ktimes[kv.first];
-        d.ms += kv.second.ms;
-        d.px += kv.second.px;
-        d.n += kv.second.n;
-      }
-      c->lanes[li - 1]->ktimes.clear();
-      c->tl.insert(c->tl.end(), c->lanes[li - 1]->tl.begin(), c->lanes[li - 1]->tl.end());
-      c->lanes[li - 1]->tl.clear();
-    }
+    merge_lane_prof(c, lanes);
     for (auto &e : errs)
       if (e.code != OF_OK) throw e;
   }
@@ -2666,12 +2678,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
     s.C = C;
   }
   lanes = std::min(lanes, npairs);
-  while ((int)c->lanes.size() < lanes - 1) {
-    of_ctx *l = nullptr;
-    const int rc = of_ctx_create(c->device, &l);
-    REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
-    c->lanes.push_back(l);
-  }
+  if (lanes > 1) ensure_lanes(c, lanes - 1);  // lane streams before the copy stream (ensure_lanes)
   for (int li = 0; li < lanes; ++li) stage_alloc(li ? c->lanes[li - 1] : c, c, 2 * (size_t)H * W * C, nu);
   if (lanes == 1) {
     run_host_lane(c, c, 0, 1, npairs, im1, im2, H, W, C, P, out_uv, st);
@@ -2703,18 +2710,7 @@ int of_pairs_run_host(of_ctx *c, int npairs, const uint8_t *const *im1, const ui
       });
     }
     for (auto &t : th) t.join();
-    c->big = nullptr;
-    for (int li = 1; li < lanes; ++li) {
-      for (auto &kv : c->lanes[li - 1]->ktimes) {
-        KTime &d = c->ktimes[kv.first];
-        d.ms += kv.second.ms;
-        d.px += kv.second.px;
-        d.n += kv.second.n;
-      }
-      c->lanes[li - 1]->ktimes.clear();
-      c->tl.insert(c->tl.end(), c->lanes[li - 1]->tl.begin(), c->lanes[li - 1]->tl.end());
-      c->lanes[li - 1]->tl.clear();
-    }
+    merge_lane_prof(c, lanes);
     for (auto &e : errs)
       if (e.code != OF_OK) throw e;
   }
@@ -2735,7 +2731,8 @@ struct PairJob {
 struct PairPool {
   int H = 0, W = 0, C = 0;
   of_params P;
-  std::vector<of_ctx *> lanes;
+  std::vector<of_ctx *> lanes;  // the ctx and its lane children (of_pairs_run's lanes), not owned
+  of_progress_fn prog_fn = nullptr;  // the ctx's progress callback, off while the pool runs
   std::vector<float *> d_uv;  // 2 device flow buffers per lane
   std::vector<std::thread> th;
   std::mutex m;
@@ -2746,6 +2743,8 @@ struct PairPool {
   std::vector<uint8_t> done;  // by ticket
   OfError err{OF_OK, ""};
 };
+
+void pool_set_progress(PairPool *pp, of_progress_fn fn) { pp->prog_fn = fn; }
 
 namespace {
 // One lane of the pool: the per-pair pipeline of run_host_lane (pinned and
@@ -2871,14 +2870,16 @@ int of_pairs_open(of_ctx *c, int H, int W, int C, const of_params *P, int lanes)
   pp->C = C;
   pp->P = *P;
   const size_t nu = 2 * (size_t)H * W;
-  stage_alloc(c, c, 0, 0);  // the shared copy stream
+  ensure_lanes(c, lanes - 1);  // lane streams before the copy stream (ensure_lanes)
   try {
+    // the pool runs on the context's long-lived lane children (the ones
+    // of_pairs_run / of_pairs_run_host use): lanes created and destroyed per
+    // pool would shift the runtime's stream -> hardware-queue mapping for
+    // the lanes created after them (create_stream)
     for (int li = 0; li < lanes; ++li) {
-      of_ctx *l = nullptr;
-      const int rc = of_ctx_create(c->device, &l);
-      REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
+      of_ctx *l = li ? c->lanes[li - 1] : c;
       pp->lanes.push_back(l);
-      l->prof = 0;
+      if (l != c) l->prof = 0;
       l->opt_sor_pipe = c->opt_sor_pipe;
       l->opt_fused_warp = c->opt_fused_warp;
       l->big = lanes > 1 && OF_BIG_PX > 0 ? &c->big_own : nullptr;
@@ -2891,12 +2892,13 @@ int of_pairs_open(of_ctx *c, int H, int W, int C, const of_params *P, int lanes)
       }
     }
   } catch (...) {
-    for (of_ctx *l : pp->lanes) of_ctx_destroy(l);
     for (float *d : pp->d_uv) hipFree(d);
     throw;
   }
   PairPool *raw = pp.release();
   c->pool = raw;
+  raw->prog_fn = c->prog_fn;  // lane 0 is the ctx: batch lanes never report
+  c->prog_fn = nullptr;
   for (int li = 0; li < lanes; ++li)
     raw->th.emplace_back([c, raw, li] {
       try {
@@ -3038,7 +3040,11 @@ int of_pairs_close(of_ctx *c) {
   }
   pp->cv_job.notify_all();
   for (auto &t : pp->th) t.join();
-  for (of_ctx *l : pp->lanes) of_ctx_destroy(l);
+  for (of_ctx *l : pp->lanes) {  // the lanes stay with the context
+    l->big = nullptr;
+    l->arena.reset();
+  }
+  c->prog_fn = pp->prog_fn;
   hipSetDevice(c->device);
   for (float *d : pp->d_uv) hipFree(d);
   const OfError e = pp->err;

@@ -82,4 +82,8 @@ out["run_first_ctx_after_pool"] = run_steps(a, K)
 c = new_ctx(2)
 out["run_third_ctx_16slots"] = run_steps(c, K)
 out["pool_third_ctx_after_run"] = pool_steps(c, K)
+out["run_third_ctx_after_its_pool"] = run_steps(c, K)
+d = new_ctx(1)
+out["run_new_ctx_after_pools"] = run_steps(d, K)
+out["run_after_pool_same_ctx_again"] = run_steps(b, K)
 print(json.dumps({k: round(v, 3) for k, v in out.items()}), flush=True)
