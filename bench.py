@@ -676,6 +676,7 @@ def main():
             "ms_per_level": [{"stage": l["stage"], "h": l["h"], "w": l["w"], "ms": round(l["ms"], 3)}
                              for l in sd["levels"]],
             "aepe_gt": round(aepe, 6),
+            "flow_sha1": __import__("hashlib").sha1(dev_uv.tobytes()).hexdigest()[:16],
             "aepe_ref": None if a_ref is None or seeds[0] != 0 else {
                 "ref_aepe_gt": round(a_ref, 6), "aepe_ref_delta": round(aepe - a_ref, 7),
                 "fixture": f"tests/golden/{ref_fix}",

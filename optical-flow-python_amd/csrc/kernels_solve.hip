@@ -1094,6 +1094,17 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 // are recorded with their measurements in DESIGN.md §3; the commits that
 // measured them hold their source.
 #define CGS_NREC 14
+// CGS_W0REG (default 1): wave 0 keeps the records of rows n-1, n-2 it
+// formed in registers instead of reading them back from the LDS ring (4
+// ds_read_b128 + 2 ds_read_b64 and their wait per row step of the
+// pace-setting wave; 184 -> 202 VGPRs, the same 2 waves / SIMD).  Round-5
+// A/B, 2 reps, the same flow bitwise (profiles/r5s_cgs_ab.log): isolated
+// 200-iteration 1080p solve 3.87 / 3.87 vs 3.96 / 3.92 ms, timed bench 47.95 /
+// 47.94 vs 47.94 / 47.87 pairs/s.  Masking the out-of-band rows instead of
+// branching over them (one basic block per row step) was 5 % slower as timed.
+#ifndef CGS_W0REG
+#define CGS_W0REG 1
+#endif
 // Waves 1 and 3 run at issue priority 1 (0 otherwise), above the
 // other lanes' kernels that share their SIMDs in the timed geometry: 45.65 /
 // 45.78 / 45.87 vs 45.34 / 45.45 / 45.57 pairs/s, 3 reps each
@@ -1208,6 +1219,16 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     q[64] = make_float4(c.wxu.y, c.wxv.y, c.wyu.y, c.wyv.y);
     q[128] = make_float4(mi.ia.x, mi.ic.x, mi.ic.x, mi.id.x);
     q[192] = make_float4(mi.ia.y, mi.ic.y, mi.ic.y, mi.id.y);
+    CgRec r;  // the record as get_rec reads it back
+    r.wx[0] = cg_f2{c.wxu.x, c.wxv.x};
+    r.wy[0] = cg_f2{c.wyu.x, c.wyv.x};
+    r.wx[1] = cg_f2{c.wxu.y, c.wxv.y};
+    r.wy[1] = cg_f2{c.wyu.y, c.wyv.y};
+    r.ma[0] = cg_f2{mi.ia.x, mi.ic.x};
+    r.mb[0] = cg_f2{mi.ic.x, mi.id.x};
+    r.ma[1] = cg_f2{mi.ia.y, mi.ic.y};
+    r.mb[1] = cg_f2{mi.ic.y, mi.id.y};
+    return r;
   };
   auto get_rec = [&](int t) {
     const float4 *q = &ring[rslot(t)][0][lane];
@@ -1290,10 +1311,13 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
     for (int m = 0; m < CGS_W2N; ++m) XI[m] = zero4;
 
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  CgRec QA[2];  // CGS_W0REG: wave 0's records of rows n - 2, n - 1 (by R2)
+  // row o inside the band (stores and dot products only there)
+  auto inband = [&](int o) { return o >= r0 && o < r1; };
   if (live) {
     if (role == 0) {
-      put_rec(ns - 2, SGp[0]);  // ring slots of rows ns - 2, ns - 1 at u = 0
-      put_rec(ns - 1, SGp[1]);
+      QA[0] = put_rec(ns - 2, SGp[0]);  // ring slots of rows ns - 2, ns - 1 at u = 0
+      QA[1] = put_rec(ns - 1, SGp[1]);
     }
     __syncthreads();
     CGS_T0
@@ -1333,16 +1357,22 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
         PO[R8(CGS_PF)] = load_po(n + CGS_PF);
         RI[RRI(CGS_PF - 1)] = load_rin(n + CGS_PF - 1);
         // A) row n-1: r = r_in - alpha A p_old, y = D^-1 r
+#if CGS_W0REG
+        const cg_f2 wu[2] = {QA[R2(-2)].wy[0], QA[R2(-2)].wy[1]};  // before row n takes the slot
+        const CgRec q1 = QA[R2(-1)];
+        QA[R2(0)] = put_rec(n, SG[RSG(0)]);
+#else
         put_rec(n, SG[RSG(0)]);
         const CgRec q1 = get_rec(n - 1);
         cg_f2 wu[2];
         get_wy(n - 2, wu);
+#endif
         cg_f4 r = RI[RRI(-1)];
         if (!FIRST) r -= alpha * (cgr_diag_raw(SG[RSG(-1)], PO[R8(-1)]) - cgr_nsum(PO[R8(-2)], PO[R8(-1)], PO[R8(0)], q1, wu));
         const cg_f4 y = cgr_minv(q1, r);
         s_y[(n - 1) & 7][lane] = make_float4(y.x, y.y, y.z, y.w);
         const int o = n - 1;
-        if (o >= r0 && o < r1) {
+        if (inband(o)) {
           cg_st4(rro, soff8 + orow(o) * rowb8, r);
           acc[4] += (double)mdot(r, r);
           acc[3] += (double)(c0 * mdot(r, y));
@@ -1413,7 +1443,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           if (!(rv && ok1)) { p.z = 0.f; p.w = 0.f; }
           PP[R4(-8)] = p;
           ZZ[R2(-8)] = z;
-          if (o >= r0 && o < r1) {
+          if (inband(o)) {
             const unsigned so = soff8 + orow(o) * rowb8;
             cg_st4(rpn, so, p);
             cg_st4(rx, so, FIRST ? zero4 : XI[RW2(-8)] + alpha * PO2[RW2(-8)]);
@@ -1431,7 +1461,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           const cg_f4 yq = cgr_minv(q5, q);
           st4(s_yq, n - 9, yq);
           const int o = n - 9;
-          if (o >= r0 && o < r1) {
+          if (inband(o)) {
             acc[0] += (double)mdot(pm, q);
             acc[1] += (double)mdot(q, ZZ[R2(-9)]);
             acc[2] += (double)(c0 * mdot(q, yq));
@@ -1456,7 +1486,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           const cg_f4 v1 = cgr_minv(q6, ny);
           V1[R4(-11)] = v1;
           const int o = n - 11;
-          if (o >= r0 && o < r1) {
+          if (inband(o)) {
             const cg_f4 t = (c1 * yq + c2 * v1) * ny;
             acc[2] += (double)((dm0 ? t.x + t.y : 0.f) + (dm1 ? t.z + t.w : 0.f));
           }
@@ -1471,7 +1501,7 @@ __global__ __launch_bounds__(256) void k_cgs(PcgArgs g, int k, int R, int nbands
           const cg_f4 vu = V2[R2(-13)];
           V2[R2(-12)] = v2;
           const int o = n - 12;
-          if (o >= r0 && o < r1) {
+          if (inband(o)) {
             const cg_f2 w0 = cg_lo(v2), w1 = cg_hi(v2);
             const cg_f2 h0 = cg_left2(q7.wx[1]) * cg_left2(w1) + wy7[0] * cg_lo(vu);
             const cg_f2 h1 = q7.wx[0] * w0 + wy7[1] * cg_hi(vu);
