@@ -1102,6 +1102,11 @@ template __global__ void k_cg_reg<0, false>(CgSmallArgs);
 // 200-iteration 1080p solve 3.87 / 3.87 vs 3.96 / 3.92 ms, timed bench 47.95 /
 // 47.94 vs 47.94 / 47.87 pairs/s.  Masking the out-of-band rows instead of
 // branching over them (one basic block per row step) was 5 % slower as timed.
+// Also measured and removed (round 5, profiles/r5u_cgs_w3rec_ab.log): the
+// coefficient loads and records moved from wave 0 to wave 3 (one row ahead,
+// a 15-row ring): wave 0 101 -> 89 K working cycles per launch but wave 3
+// 56 -> 92 K, a 200-iteration 1080p solve 4.19 vs 3.90 ms, 45.0 vs 47.8
+// pairs/s, the same flow bitwise.
 #ifndef CGS_W0REG
 #define CGS_W0REG 1
 #endif
