@@ -955,6 +955,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       lstu = ina[i] ? qa[i] : lstu;
       lstv = inb[i] ? qv[i] : lstv;
     }
+    // (measured r5v: a wave-level exit once every lane has both medians,
+    // `if (!__any(resu == 0xffff || resv == 0xffff)) break;`, is 1.5 % slower
+    // per launch, 0.812 vs 0.801 ms, same flow: the walk is short and the
+    // vote costs more than the samples it saves)
   }
   if (resu == 0xffffu) resu = lstu;
   if (resv == 0xffffu) resv = lstv;
