@@ -678,10 +678,12 @@ __device__ __forceinline__ void swap_lane64(uint64_t v, int lj, uint64_t &a, uin
 // every finite fp32) so no key is a NaN, padding to 2^1002.  The position is
 // the key's low 16 bits either way.
 __device__ __forceinline__ uint64_t wmf_key(float v, unsigned pos) {
-  double d = (double)v;
-  if (__builtin_isnan(v)) d = 0x1p1001;
-  else if (__builtin_isinf(v)) d = v > 0.f ? 0x1p1000 : -0x1p1000;
-  return __builtin_bit_cast(uint64_t, d) | (uint64_t)pos;
+  // selects, not branches: the region load issues every read before the
+  // first key is formed
+  const double d = (double)v;
+  const double e = v > 0.f ? 0x1p1000 : -0x1p1000;
+  const double f = __builtin_isnan(v) ? 0x1p1001 : (__builtin_isinf(v) ? e : d);
+  return __builtin_bit_cast(uint64_t, f) | (uint64_t)pos;
 }
 #define WMF_PAD_KEY (__builtin_bit_cast(uint64_t, 0x1p1002) | 0xffffull)
 __device__ __forceinline__ double wmf_d(uint64_t k) { return __builtin_bit_cast(double, k); }
@@ -807,24 +809,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const int ty0 = tby * WMF_T, tx0 = tbx * WMF_T;
   const int lane = threadIdx.x;
   WMF_STAMP(0);
+  // region load: every lane's NPER samples' offsets first (padding lanes,
+  // s >= nreg, re-read the last sample and rewrite its record with the same
+  // bytes), then all uv / guide / occ reads, then keys and records -- no
+  // branch between the reads, so they are all in flight at once (was one
+  // round trip per sample and read kind: 15.5 K of 102 K cycles per wave)
   uint64_t a[NPER], b[NPER];
+  unsigned goff[NPER], rpos[NPER];
+  auto region_offsets = [&](auto mirf) {
+#pragma unroll
+    for (int r = 0; r < NPER; ++r) {
+      const int s = min(lane * NPER + r, nreg - 1);
+      const int ry = s / RW, rx = s - ry * RW;
+      goff[r] = (unsigned)(mirf(ty0 - hsz + ry, H) * P + mirf(tx0 - hsz + rx, W));
+      rpos[r] = ((unsigned)ry << 8) | (unsigned)rx;
+    }
+  };
+  if (fold1)
+    region_offsets([](int i, int n) { return i < 0 ? -i : (i >= n ? 2 * (n - 1) - i : i); });
+  else
+    region_offsets([](int i, int n) { return ext_mirror(i, n); });
+  float2 rv[NPER];
+  float rg[NPER][3], ro[NPER];
+#pragma unroll
+  for (int r = 0; r < NPER; ++r) rv[r] = uv[goff[r]];
 #pragma unroll
   for (int r = 0; r < NPER; ++r) {
-    const int s = lane * NPER + r;
-    a[r] = WMF_PAD_KEY;
-    b[r] = WMF_PAD_KEY;
-    if (s < nreg) {
-      const int ry = s / RW, rx = s - ry * RW;
-      const size_t g = (size_t)mir(ty0 - hsz + ry, H) * P + mir(tx0 - hsz + rx, W);
-      const float2 v = uv[g];
-      const unsigned lo = ((unsigned)ry << 8) | (unsigned)rx;
-      a[r] = wmf_key(v.x, lo);
-      b[r] = wmf_key(v.y, lo);
-      float gv[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < GC; ++c) gv[c] = guide[c * ps + g];
-      smp[ry * RP + rx] = WmfRec<GC>::make(gv[0], gv[1], gv[2], occ[g]);
-    }
+    for (int c = 0; c < 3; ++c) rg[r][c] = c < GC ? guide[c * ps + goff[r]] : 0.f;
+    ro[r] = occ[goff[r]];
+  }
+#pragma unroll
+  for (int r = 0; r < NPER; ++r) {
+    // padding keys by a mask, not a select: a per-lane select lets the
+    // compiler sink the last sample's read into a branch behind the others
+    const uint64_t pm = 0ull - (uint64_t)(lane * NPER + r >= nreg);
+    const uint64_t ka = wmf_key(rv[r].x, rpos[r]), kb = wmf_key(rv[r].y, rpos[r]);
+    a[r] = ka ^ ((ka ^ WMF_PAD_KEY) & pm);
+    b[r] = kb ^ ((kb ^ WMF_PAD_KEY) & pm);
+    smp[(rpos[r] >> 8) * RP + (rpos[r] & 0xffu)] = WmfRec<GC>::make(rg[r][0], rg[r][1], rg[r][2], ro[r]);
   }
   wmf_sum_t *cs = csum + lane;
 #pragma unroll

@@ -33,7 +33,7 @@ int main() {
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int rep = 0; rep < 3; ++rep) {
     hipEventRecord(e0);
-    hipLaunchKernelGGL((k_wmf<3, 8, 7>), grid, dim3(64), shm, 0, uv, g, o, out, H, W, P, ps, hsz, nk, RW, RP);
+    hipLaunchKernelGGL((k_wmf<3, 8, 7>), grid, dim3(64), shm, 0, uv, g, o, out, H, W, P, ps, hsz, nk, RW, RP, (const float2 *)nullptr);
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     std::vector<unsigned long long> t(32400 * 8);
