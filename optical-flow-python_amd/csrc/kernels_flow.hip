@@ -701,70 +701,119 @@ __device__ __forceinline__ uint64_t wmf_max(uint64_t a, uint64_t b) {
   return __builtin_bit_cast(uint64_t, r);
 }
 
-// Bitonic sort of the 64*NPER keys of two lists at once (element e = lane *
-// NPER + r).  Merge kk sorts blocks of kk elements ascending where e & kk is
-// 0 and descending elsewhere; here the keys of descending blocks carry a
-// flipped sign bit during that merge (min of negated keys = max), so every
-// compare-exchange is ascending: a pair inside a lane is one v_min_f64 +
-// one v_max_f64 (was v_cmp_u64 + four v_cndmask), and only the lower lane of
-// a cross-lane pair keeps the minimum.  The sign flips between merges cost one
-// v_xor per key where the block direction changes.  Partners at distance
-// >= NPER are in another lane (xor_lane64 / v_permlane{16,32}_swap).
+// (min, max) of a pair from one asm statement: a select between two outputs
+// of one statement cannot be turned into a branch around either
+__device__ __forceinline__ void wmf_minmax(uint64_t a, uint64_t b, uint64_t &mn, uint64_t &mx) {
+  double r0, r1;
+  asm("v_min_f64 %0, %2, %3\n\tv_max_f64 %1, %2, %3" : "=&v"(r0), "=&v"(r1) : "v"(wmf_d(a)), "v"(wmf_d(b)));
+  mn = __builtin_bit_cast(uint64_t, r0);
+  mx = __builtin_bit_cast(uint64_t, r1);
+}
+// min(a, -b) in one v_min_f64 (source negate modifier)
+__device__ __forceinline__ uint64_t wmf_min_neg(uint64_t a, uint64_t b) {
+  double r;
+  asm("v_min_f64 %0, %1, -%2" : "=v"(r) : "v"(wmf_d(a)), "v"(wmf_d(b)));
+  return __builtin_bit_cast(uint64_t, r);
+}
+
 template <int NPER>
-__device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&kb)[NPER], int lane) {
-  constexpr int N = NPER * 64;
-#pragma unroll
-  for (int kk = 2; kk <= N; kk <<= 1) {
-    // sign of element e in merge kk: (e & kk) != 0; flip where it differs
-    // from merge kk/2's (no sign before the first merge)
+struct Bitonic {
+  static constexpr int N = NPER * 64;
+  // lane bits of the sign in stage (kk, jj): (lane * NPER) & kk, xor lj for a
+  // DPP cross-lane stage; and the bit of r (kk < NPER)
+  static constexpr int lane_sel(int kk, int jj) {
+    return ((kk >= NPER ? kk / NPER : 0) ^ (jj >= NPER && jj / NPER < 16 ? jj / NPER : 0)) & 63;
+  }
+  static constexpr bool r_bit(int r, int kk) { return kk < NPER && (r & kk) != 0; }
+
+  // one stage (kk, jj) after stage (pkk, pjj) (pkk = 0: none), then the next
+  template <int KK, int JJ, int PKK, int PJJ>
+  __device__ __forceinline__ static void stage(uint64_t (&ka)[NPER], uint64_t (&kb)[NPER], int lane) {
+    constexpr int ls = lane_sel(KK, JJ) ^ (PKK ? lane_sel(PKK, PJJ) : 0);
+    const unsigned lflip = ls ? (unsigned)(__builtin_popcount(lane & ls) & 1) << 31 : 0u;
 #pragma unroll
     for (int r = 0; r < NPER; ++r) {
-      const int e0 = lane * NPER + r;
-      const bool s_now = (e0 & kk) != 0, s_prev = kk > 2 && (e0 & (kk >> 1)) != 0;
-      const uint64_t m = (uint64_t)(s_now != s_prev) << 63;
-      ka[r] ^= m;
-      kb[r] ^= m;
+      const bool rf = r_bit(r, KK) != (PKK ? r_bit(r, PKK) : false);
+      if (ls || rf) {
+        const uint64_t m = (uint64_t)(lflip ^ (rf ? 0x80000000u : 0u)) << 32;
+        ka[r] ^= m;
+        kb[r] ^= m;
+      }
     }
-#pragma unroll
-    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-      if (jj >= NPER) {
-        const int lj = jj / NPER;
+    if constexpr (JJ >= NPER) {
+      constexpr int lj = JJ / NPER;
+      if constexpr (lj == 16 || lj == 32) {
         const bool take_min = (lane & lj) == 0;
-        if (lj == 16 || lj == 32) {
-          // v_permlane{16,32}_swap of a value with itself leaves (own, partner)
-          // in the two outputs, in a lane-dependent order; min / max of the
-          // pair is order-free, so no select of the partner is needed
 #pragma unroll
-          for (int r = 0; r < NPER; ++r) {
-            uint64_t p0, p1, q0, q1;
-            swap_lane64(ka[r], lj, p0, p1);
-            swap_lane64(kb[r], lj, q0, q1);
-            ka[r] = ((wmf_d(p0) < wmf_d(p1)) == take_min) ? p0 : p1;
-            kb[r] = ((wmf_d(q0) < wmf_d(q1)) == take_min) ? q0 : q1;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < NPER; ++r) {
-            const uint64_t oa = xor_lane64(ka[r], lj), ob = xor_lane64(kb[r], lj);
-            ka[r] = ((wmf_d(ka[r]) < wmf_d(oa)) == take_min) ? ka[r] : oa;
-            kb[r] = ((wmf_d(kb[r]) < wmf_d(ob)) == take_min) ? kb[r] : ob;
-          }
+        for (int r = 0; r < NPER; ++r) {
+          uint64_t p0, p1, q0, q1, an, ax, bn, bx;
+          swap_lane64(ka[r], lj, p0, p1);
+          swap_lane64(kb[r], lj, q0, q1);
+          wmf_minmax(p0, p1, an, ax);
+          wmf_minmax(q0, q1, bn, bx);
+          ka[r] = take_min ? an : ax;
+          kb[r] = take_min ? bn : bx;
         }
       } else {
 #pragma unroll
         for (int r = 0; r < NPER; ++r) {
-          const int rp = r ^ jj;
-          if (rp > r) {
-            const uint64_t a0 = ka[r], a1 = ka[rp], b0 = kb[r], b1 = kb[rp];
-            ka[r] = wmf_min(a0, a1);
-            ka[rp] = wmf_max(a0, a1);
-            kb[r] = wmf_min(b0, b1);
-            kb[rp] = wmf_max(b0, b1);
-          }
+          ka[r] = wmf_min_neg(ka[r], xor_lane64(ka[r], lj));
+          kb[r] = wmf_min_neg(kb[r], xor_lane64(kb[r], lj));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < NPER; ++r) {
+        const int rp = r ^ JJ;
+        if (rp > r) {
+          const uint64_t a0 = ka[r], a1 = ka[rp], b0 = kb[r], b1 = kb[rp];
+          ka[r] = wmf_min(a0, a1);
+          ka[rp] = wmf_max(a0, a1);
+          kb[r] = wmf_min(b0, b1);
+          kb[rp] = wmf_max(b0, b1);
+        }
+      }
+    }
+    if constexpr (JJ > 1) {
+      stage<KK, JJ / 2, KK, JJ>(ka, kb, lane);
+    } else if constexpr (KK < N) {
+      stage<2 * KK, KK, KK, JJ>(ka, kb, lane);
+    } else {
+      // back to plain keys (the last merge's blocks are all ascending and
+      // its last stage is in-lane: nothing left to flip unless NPER == 1)
+      constexpr int le = lane_sel(KK, JJ);
+      if constexpr (le != 0) {
+        const uint64_t m = (uint64_t)((unsigned)(__builtin_popcount(lane & le) & 1) << 31) << 32;
+#pragma unroll
+        for (int r = 0; r < NPER; ++r) {
+          ka[r] ^= m;
+          kb[r] ^= m;
         }
       }
     }
   }
+};
+
+// Bitonic sort of the 64*NPER keys of two lists at once (element e = lane *
+// NPER + r).  Merge kk sorts blocks of kk elements ascending where e & kk is
+// 0 and descending elsewhere; the keys of descending blocks carry a flipped
+// sign bit during that merge (min of negated keys = max), so every
+// compare-exchange is ascending.  A pair inside a lane is one v_min_f64 + one
+// v_max_f64.  A pair across lanes at lane distance lj < 16 (DPP partner):
+// during that stage the upper lane of each pair (lane & lj) holds its keys
+// negated as well, so both lanes compute min(own, -partner) -- the lower lane
+// gets min(x_L, x_U), the upper -max(x_L, x_U) -- one v_min_f64 with a
+// negated source and no per-lane select (was v_cmp + an SALU xor of the
+// compare mask with the lane's direction + two v_cndmask, the compare mask
+// one SGPR pair every key waited on).  The sign changes between stages are
+// one v_xor of the high dword per key with a lane-only mask (Bitonic::stage:
+// every stage a template instance, so every mask and partner distance is a
+// compile-time constant).  At lj = 16 / 32 (v_permlane{16,32}_swap: own and
+// partner in a lane-dependent order) both lanes form min and max and keep
+// one by a lane-constant mask.
+template <int NPER>
+__device__ __forceinline__ void bitonic_regs2(uint64_t (&ka)[NPER], uint64_t (&kb)[NPER], int lane) {
+  Bitonic<NPER>::template stage<2, 1, 0, 0>(ka, kb, lane);
 }
 
 // HS > 0: area_hsz fixed at compile time (window loop fully unrolled,
