@@ -74,7 +74,10 @@ KERNEL_BYTES_PER_PX = {
 }
 # VALU issue peak (MI355X_MICROARCH.md: a wave issues one VALU instruction per
 # 2 cycles per SIMD; 256 CUs x 4 SIMDs at 2.4 GHz): wave-instructions / s
-VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9
+CLOCK_HZ = 2.4e9
+VALU_ISSUE_PEAK = 256 * 4 * 0.5 * CLOCK_HZ
+# the weighted median's per-phase ISA census priced by measured issue costs
+WMF_CENSUS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5_wmf_census.json")
 
 
 def parse():
@@ -240,10 +243,13 @@ def ref_aepe():
 
 
 def wmf_compute_roofline(per_level):
-    """The weighted median is VALU-issue bound, not HBM bound (SURVEY.md
-    §8d): VALU wave-instructions per finest-level launch (SQ_INSTS_VALU, PMC
-    pass of tools/profile.sh) / that launch's mean duration in the isolated
-    replay, against the chip's VALU issue rate (VALU_ISSUE_PEAK)."""
+    """The weighted median is not HBM bound: `frac` = the
+    VALU SIMD-cycles its instructions occupy (tools/isa_census.py: the
+    shipped ISA per phase, each opcode at its measured issue cost,
+    profiles/r5_wmf_census.json) over the finest-level launch's mean duration
+    in the isolated replay x 1024 SIMDs x clock.  Beside it the PMC
+    instruction rate against a 2-cycle issue (`insts_frac_2cyc`, which
+    understates fp64 / transcendental / DPP instructions) and `hbm_frac`."""
     rec = load_pmc("wmf")
     lv = [(px, r) for (n, px), r in per_level.items() if n == "wmf"]
     if not lv:
@@ -258,11 +264,27 @@ def wmf_compute_roofline(per_level):
         ach = vi / (ms * 1e-3)
         out.update({"valu_insts_per_launch": vi, "valu_insts_per_px": round(vi * 64 / px, 1),
                     "achieved": round(ach / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
-                    "unit": "G wave-instr/s", "frac": round(ach / VALU_ISSUE_PEAK, 4)})
+                    "unit": "G wave-instr/s", "insts_frac_2cyc": round(ach / VALU_ISSUE_PEAK, 4)})
     if rec.get("valu_pipe_busy") is not None:
         # issue counts price every instruction at 2 cycles; the SQ's active
         # cycles (fp64, transcendental, 64-bit ops take longer) give the pipe
         out.update({"valu_pipe_busy": rec["valu_pipe_busy"], "valu_pipe_busy_source": rec.get("sq_source")})
+    try:
+        cen = json.load(open(WMF_CENSUS))
+    except (OSError, ValueError):
+        cen = None
+    if cen:
+        # the headline figure: VALU SIMD-cycles per wave from the ISA census
+        # (tools/isa_census.py: every opcode priced by its measured issue cost
+        # at the kernel's 2 waves per SIMD, tools/micro/valu_cost.hip) x one
+        # wave per 8x8 tile / (1024 SIMDs x clock x launch time)
+        waves = -(-px // 64)
+        simd_s = cen["total"]["valu_simd_cycles"] * waves / (256 * 4) / CLOCK_HZ
+        out.update({"valu_simd_cycles_per_wave": cen["total"]["valu_simd_cycles"],
+                    "valu_insts_per_wave_isa": cen["total"]["valu"],
+                    "frac": round(simd_s / (ms * 1e-3), 4),
+                    "frac_basis": "VALU SIMD-cycles at measured issue costs / launch time "
+                                  "(" + os.path.relpath(WMF_CENSUS, ROOT) + ")"})
     return out
 
 
