@@ -852,9 +852,13 @@ void cheb_poly(int m, double a, double b, double *cB) {
 #define CG_CHEB_A 0.04
 // the robust GNC stages (alpha < 0.5: D^-1 A with more small eigenvalues):
 // 0.02 takes 479 instead of 488 CG iterations per 1080p pair (+1.5 %
-// pairs/s; profiles/r3q_cheb_robust_ab.log)
+// pairs/s; profiles/r3q_cheb_robust_ab.log); 0.01 476 (49.72 / 49.83 vs
+// 49.25 / 49.35 pairs/s, parity suites green; profiles/r5aa_cheb01_ab.log).
+// Offline at 540p (tools/poly_iters.py's operator): 56 / 54 / 52 / 52
+// iterations at 0.04 / 0.02 / 0.01 / 0.005; least-squares polynomials of the
+// same degree 62-73; an upper end below 2 makes p negative on the spectrum
 #ifndef CG_CHEB_A_ROBUST
-#define CG_CHEB_A_ROBUST 0.02
+#define CG_CHEB_A_ROBUST 0.01
 #endif
 
 // Launch geometry of the fused CG iteration kernels for an H x W level.
