@@ -656,6 +656,11 @@ static int sor(const double *coef, const double *b, int H, int W, double omega, 
  * rtol from fp32 arithmetic; <= 0 restores 1e-12. */
 static double g_backslash_rtol = 1e-12;
 void ofr_set_backslash_rtol(double rtol) { g_backslash_rtol = rtol > 0 ? rtol : 1e-12; }
+/* ofr_set_round_x_f32 (test-only experiment knob, tools/rtol_chaos.py): round
+ * every 'backslash' solution to float32, as the GPU returns it, to measure
+ * what fp32 storage of x alone does to the chaotic family. */
+static int g_round_x_f32 = 0;
+void ofr_set_round_x_f32(int on) { g_round_x_f32 = on != 0; }
 
 int ofr_solve(const of_params *P, const double *coef, const double *rhs, int H, int W, double *x, int *iters,
               double *relres) {
@@ -663,7 +668,11 @@ int ofr_solve(const of_params *P, const double *coef, const double *rhs, int H, 
   int it;
   if (P->solver == OF_SOLVER_PCG) it = pcg(coef, rhs, H, W, P->pcg_rtol, P->pcg_maxiter, 0, x, &rr);
   else if (P->solver == OF_SOLVER_SOR) it = sor(coef, rhs, H, W, 1.9, P->sor_max_iters, 1e-2, x);
-  else it = pcg(coef, rhs, H, W, g_backslash_rtol, 100000, 1, x, &rr);
+  else {
+    it = pcg(coef, rhs, H, W, g_backslash_rtol, 100000, 1, x, &rr);
+    if (g_round_x_f32)
+      for (long k = 0; k < 2L * H * W; ++k) x[k] = (double)(float)x[k];
+  }
   if (iters) *iters = it;
   if (relres) *relres = rr;
   return 0;

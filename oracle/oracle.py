@@ -44,6 +44,7 @@ def lib():
         _lib.ofr_solve.argtypes = [C.POINTER(_abi.OfParams), _dp, _dp, C.c_int, C.c_int, _dp, _ip, _dp]
         _lib.ofr_num_threads.restype = C.c_int
         _lib.ofr_set_backslash_rtol.argtypes = [C.c_double]
+        _lib.ofr_set_round_x_f32.argtypes = [C.c_int]
     return _lib
 
 
@@ -70,6 +71,12 @@ def set_backslash_rtol(rtol):
     """Test-only: stop the oracle's 'backslash' PCG at `rtol` instead of 1e-12
     (None or <= 0 restores 1e-12).  Process-global."""
     lib().ofr_set_backslash_rtol(C.c_double(float(rtol or 0.0)))
+
+
+def set_round_x_f32(on):
+    """Test-only experiment knob (tools/rtol_chaos.py): round every
+    'backslash' solution to float32, as the GPU returns it."""
+    lib().ofr_set_round_x_f32(C.c_int(1 if on else 0))
 
 
 def num_threads():

@@ -77,11 +77,28 @@ def test_e2e_synthetic(golden, method):
     """synth_pair(120, 160, 0) end to end vs the reference.  Chaotic methods
     are gated at 1.5x the reference's own spread under a float32-level (6e-8
     relative) perturbation of its gray input (max over 3 seeds,
-    chaos_synth.npz): an fp32 implementation IS such a perturbation.  The
-    1e-12 spread is printed beside; measured (round 4) classic-c 2.0e-2 /
-    1.33e-2 vs the reference's 6e-8 spread 2.1e-2 / 1.43e-2 (1e-12: 1.4e-2 /
-    8.8e-3), classic++ 1.97e-2 / 1.04e-2 vs 2.0e-2 / 9.8e-3 (1e-12: 8.9e-3 /
-    4.6e-3).  Other methods by TOL."""
+    chaos_synth.npz).  The 1e-12 spread is printed beside; measured (round 4)
+    classic-c 2.0e-2 / 1.33e-2 vs the reference's 6e-8 spread 2.1e-2 /
+    1.43e-2 (1e-12: 1.4e-2 / 8.8e-3), classic++ 1.97e-2 / 1.04e-2 vs 2.0e-2 /
+    9.8e-3 (1e-12: 8.9e-3 / 4.6e-3).
+
+    What the gap is made of (round 5; tools/rtol_chaos.py,
+    profiles/r5_rtol_chaos.jsonl, mean EPE to the reference, classic-c /
+    classic++): the fp64 oracle with its 'backslash' stopped at the GPU's
+    1e-6 lands where the GPU does, 1.98e-2 / 2.11e-2; stopped at 1e-12 it is
+    at 1.22e-2 / 0.50e-2, at 1e-8 1.77e-2 / 1.61e-2.  With every solution
+    rounded to float32 (the form the GPU returns x in) and solved to 1e-12:
+    1.76e-2 / 1.34e-2.  On the GPU, solving every level <= 65536 px 100x
+    tighter (1e-8) moved the flow only to 1.85e-2 / 1.96e-2
+    (profiles/r5ab_small_rtol_probe.log): the fp32 CG's returned x has a true
+    residual of ~1e-7 however far its iterate goes (k_cg_reg iterate 6e-9,
+    returned x 3e-8 .. 2e-7; k_cgs quadratic-stage solves 9e-8 with an
+    estimate of 4e-9), and at 1e-7 the fp64 oracle is already at 2.0e-2 /
+    1.78e-2.  So below the 1e-6 stop the limit is fp32 -- x and the flow
+    state it updates -- and 2x the reference's 1e-12 spread (2.8e-2 /
+    1.78e-2) is out of reach for classic++ without fp64 solves and flow
+    state; the gate stays at the reference's float32-level spread.  Other
+    methods by TOL."""
     import optical_flow
     d = golden("e2e_synth.npz")
     ch = golden("chaos_synth.npz")

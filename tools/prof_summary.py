@@ -22,6 +22,12 @@ def short(name):
     """kernel family: template variants of the CG / weighted-median kernels
     (first launch, odd width; guide channels) are one kernel here"""
     n = name.split("(")[0].replace("void ", "")
+    # the assembly kernels' penalty-mode instances are one kernel; the fused
+    # warp + assembly keeps its interpolation (different bytes per pixel)
+    if n.startswith("k_flow_operator<"):
+        return "k_flow_operator"
+    if n.startswith("k_warp_operator<"):
+        return "k_warp_operator<" + n[len("k_warp_operator<"):].split(",")[0].strip() + ">"
     for fam in ("k_cgs", "k_cgp", "k_cgn", "k_cg_small", "k_cg<", "k_wmf"):
         if n.startswith(fam):
             return fam.rstrip("<")
@@ -120,7 +126,9 @@ def main():
             rec["l2_hit"] = round(sum(hk) / (sum(hk) + sum(mk)), 3)
         key = {"k_cgs": "pcg_iter", "k_cgp": "pcg_iter", "k_cg": "pcg_iter", "k_flow_operator": "flow_operator",
                "k_wmf": "wmf", "k_rof_iters": "rof_iters", "k_update_occ": "update_occ",
-               "k_partial_deriv<1>": "partial_deriv_hermite", "k_sor_pipe": "sor_pipe", "k_sor_lex": "sor_sweep"}.get(n)
+               "k_partial_deriv<1>": "partial_deriv_hermite", "k_sor_pipe": "sor_pipe", "k_sor_lex": "sor_sweep",
+               "k_warp_operator<1>": "warp_operator_hermite", "k_warp_operator<0>": "warp_operator_bspline",
+               "k_warp_operator<2>": "warp_operator_bilinear"}.get(n)
         if key in bench.KERNEL_BYTES_PER_PX:
             px = a.H * a.W * (2 if key == "rof_iters" else 1)
             alg = bench.KERNEL_BYTES_PER_PX[key] * px

@@ -18,7 +18,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 S="bench.py $EXTRA --steps 1 --warmup 0 --pairs 1 --lanes 1 --no-cpu-baseline --no-profile --no-stream"
-KRE='k_cgs|k_cgp|k_cg<|k_wmf|k_flow_operator|k_partial_deriv|k_rof_iters|k_update_occ|k_sor_pipe'
+KRE='k_cgs|k_cgp|k_cg<|k_wmf|k_flow_operator|k_warp_operator|k_partial_deriv|k_rof_iters|k_update_occ|k_sor_pipe'
 tools/gpu_step.sh 400 $OUT/trace.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace -- python3 bench.py $EXTRA --no-cpu-baseline || exit $?
 tools/gpu_step.sh 400 $OUT/trace1.log rocprofv3 --kernel-trace --stats -f csv -d $OUT -o trace1 -- python3 bench.py $EXTRA --lanes 1 --no-cpu-baseline --no-profile --no-stream || exit $?
 tools/gpu_step.sh 300 $OUT/fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT -o fetch -- python3 $S || exit $?
