@@ -191,3 +191,19 @@ static inline Grid2 grid2(int H, int W, int max_blocks = 2048) {
 #define OF_FOR_PIXELS(H, W)                                        \
   const int j = blockIdx.x * OF_BX + threadIdx.x;                  \
   for (int i = blockIdx.y * OF_BY + threadIdx.y; i < (H); i += gridDim.y * OF_BY)
+
+// The same loop with an XCD-aware block order, for stencil / gather kernels
+// whose blocks read their neighbours' rows: workgroups b, b + 8, b + 16 ...
+// run on one XCD (one L2), so each XCD gets a contiguous range of the grid's
+// row-major blocks and vertically / horizontally adjacent blocks share their
+// halo rows in one L2 instead of fetching them from HBM twice.  A permutation
+// of the blocks: every pixel is still visited once, by one thread.
+__device__ __forceinline__ int of_xcd_tile(int lin, int nt) {
+  const int xcd = lin & 7;
+  return xcd * (nt >> 3) + min(xcd, nt & 7) + (lin >> 3);
+}
+#define OF_FOR_PIXELS_XCD(H, W)                                                                       \
+  const int of_t_ = of_xcd_tile(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);         \
+  const int of_by_ = of_t_ / (int)gridDim.x;                                                          \
+  const int j = (of_t_ - of_by_ * (int)gridDim.x) * OF_BX + threadIdx.x;                              \
+  for (int i = of_by_ * OF_BY + threadIdx.y; i < (H); i += gridDim.y * OF_BY)

@@ -152,7 +152,7 @@ template <int INTERP>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_partial_deriv(DerivArgs d, const float2 *__restrict__ uv, int H,
                                                                 int W, int P, size_t ps, float *__restrict__ It,
                                                                 float *__restrict__ Ix, float *__restrict__ Iy) {
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     float2 f = uv[k];
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
                                 const float *__restrict__ It, const float *__restrict__ Ix, const float *__restrict__ Iy,
                                 int nc, const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     assemble_px<0, M>(o, uv, duv, nc, uvhat, i, j, H, W, P, ps, coef, rhs, [&](int ch, float &it, float &gx, float &gy) {
@@ -285,7 +285,7 @@ template <int INTERP, int NC, int M>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_warp_operator(DerivArgs d, OpArgs o, const float2 *__restrict__ uv,
                                                                 int H, int W, int P, size_t ps,
                                                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     const float2 f = uv[k];
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator_f64(OpArgs o, co
                                 const float *__restrict__ Ix, const float *__restrict__ Iy, int nc,
                                 const float2 *__restrict__ uvhat, int H, int W, int P, size_t ps,
                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     const double2 c = ld_uvd_f64(uv, duv, k);
@@ -404,7 +404,7 @@ __device__ __forceinline__ float2 upd(const float2 *uv, const float2 *x, size_t 
 __global__ void k_update_occ(const float2 *__restrict__ uv, const float2 *__restrict__ x, int clip,
                              float2 *__restrict__ uv1, const float *__restrict__ I1, const float *__restrict__ I2,
                              int nc, float *__restrict__ occ, int H, int W, int P, size_t ps) {
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const size_t k = (size_t)i * P + j;
     const float2 c = upd(uv, x, k, clip);
@@ -483,7 +483,7 @@ __device__ __forceinline__ float median_window(const float *a) {
 template <int S>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_median2(const float2 *__restrict__ in, float2 *__restrict__ out, int H, int W, int P) {
   constexpr int h = S / 2;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     float au[S * S], av[S * S];
     int t = 0;
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_median1(const float *__restric
   constexpr int h = S / 2;
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     float a[S * S];
     int t = 0;
