@@ -36,7 +36,7 @@ def test_phases_in_order(wmf):
     assert starts == sorted(starts)
     assert ph["walk"][1] == 8
     ops = [o for _, o, _ in ins]
-    assert sum(1 for i in ph["window"][0] if ops[i] == "ds_add_f64") == 2 * 15 * 15
+    assert sum(1 for i in ph["window"][0] if ops[i] in ("ds_add_u64", "ds_add_f64")) == 2 * 15 * 15
 
 
 def test_region_reads_before_first_wait(wmf):

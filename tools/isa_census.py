@@ -9,7 +9,7 @@ ships, priced with measured issue costs.
      keys, records; the general-mirror arm, only taken on planes smaller than
      the tile + window, is left out), sort (up to the first ds_write_b16 of
      the sorted positions), scatter (positions and chunk ids), window (to the
-     last ds_add_f64), chunk (prefix sums), walk (the loop body x its trip
+     last chunk-sum atomic, ds_add_u64 / ds_add_f64), chunk (prefix sums), walk (the loop body x its trip
      count CH / 8 = 8), epilogue;
   3. each VALU opcode priced by tools/micro/valu_cost.hip's measurement
      (profiles/r5w_valu_cost.json, column w2: wave-cycles per instruction with
@@ -155,7 +155,7 @@ def phases(ins):
     zero = last(lambda i: ops[i].startswith("ds_write2st64_b64"))  # chunk sums cleared: end of load
     scat = first(lambda i: ops[i] == "ds_write_b16", zero)
     win = first(lambda i: ops[i].startswith("ds_read_b") and ops[i] != "ds_read_b16", scat)
-    wend = last(lambda i: ops[i] == "ds_add_f64")
+    wend = last(lambda i: ops[i] in ("ds_add_f64", "ds_add_u64"))
     # the walk: the backward branch after the window pass
     back = None
     for i in range(wend, len(ins)):
