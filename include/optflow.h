@@ -184,6 +184,10 @@ int of_set_option(of_ctx *ctx, int option, int value);
  *                         and were redone by the per-sweep kernel (the same
  *                         result; a sign of an oversubscribed GPU) */
 #define OF_OPT_SOR_FALLBACKS 2
+/*   OF_OPT_DEVICE_BYTES   device bytes the context and its batch lanes hold in
+ *                         grow-only buffers (arena, SOR sweep ring, gather
+ *                         buffer): flat across repeated pairs of one size */
+#define OF_OPT_DEVICE_BYTES 4
 int of_get_option(of_ctx *ctx, int option, int64_t *value);
 /* progress of compute_flow / compute_flow_base: the reference's `display`
  * prints and its per-GNC-stage report (classic_nl.py:141-196, 255-256;

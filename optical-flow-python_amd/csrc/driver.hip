@@ -100,6 +100,11 @@ struct Arena {
     for (auto &c : chunks) hipFree(c.p);
     chunks.clear();
   }
+  size_t reserved() const {
+    size_t n = 0;
+    for (const auto &c : chunks) n += c.cap;
+    return n;
+  }
 };
 
 struct Img {  // C planar pitched fp32 planes
@@ -2161,6 +2166,17 @@ int of_get_option(of_ctx *c, int option, int64_t *value) {
     case OF_OPT_SOR_FALLBACKS: {
       int64_t n = c->sor_fallbacks;
       for (of_ctx *l : c->lanes) n += l->sor_fallbacks;
+      *value = n;
+      return OF_OK;
+    }
+    case OF_OPT_DEVICE_BYTES: {
+      // grow-only device buffers of the context and its lanes: the arena
+      // chunks, the pipelined SOR's sweep ring and the RCCL gather buffer
+      auto held = [](const of_ctx *x) {
+        return (int64_t)(x->arena.reserved() + x->sor_ring_cap + x->gather_cap);
+      };
+      int64_t n = held(c);
+      for (of_ctx *l : c->lanes) n += held(l);
       *value = n;
       return OF_OK;
     }

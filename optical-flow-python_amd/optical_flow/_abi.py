@@ -22,6 +22,7 @@ MAX_LEVELS = 32
 OF_OPT_SOR_PIPELINE = 1  # of_set_option
 OF_OPT_SOR_FALLBACKS = 2  # of_get_option (read-only counter)
 OF_OPT_FUSED_WARP = 3  # of_set_option: warp + assembly in one kernel (default 1)
+OF_OPT_DEVICE_BYTES = 4  # of_get_option (read-only): grow-only device bytes of the context and its lanes
 
 
 class OfPenalty(C.Structure):

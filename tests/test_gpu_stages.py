@@ -233,6 +233,26 @@ def test_sor_pipelined_bitwise_e2e(golden):
     np.testing.assert_array_equal(uv1, uv0)
 
 
+def test_sor_device_memory_flat(golden):
+    """the pipelined SOR's ring of sweep buffers is one grow-only
+    buffer per context (was carved from the per-pair arena on every solve:
+    one more ring per warp / level).  HS with 'sor' end to end, three times
+    in one context: the context's device bytes (OF_OPT_DEVICE_BYTES: arena
+    chunks + SOR ring + gather buffer) do not grow after the first call, and
+    no pipelined solve fell back to the per-sweep kernel."""
+    import optical_flow
+    from optical_flow import _abi, _native
+    d = golden("e2e_synth.npz")
+    ctx = _native.context()
+    held = []
+    for _ in range(3):
+        optical_flow.estimate_flow(d["im1"], d["im2"], "hs", {"solver": "sor"})
+        held.append(ctx.get_option(_abi.OF_OPT_DEVICE_BYTES))
+    print("device bytes per call", held)
+    assert held[0] > 0 and held[1] == held[0] and held[2] == held[0], held
+    assert ctx.get_option(_abi.OF_OPT_SOR_FALLBACKS) == 0
+
+
 def test_occlusion(golden):
     from optical_flow.utils.occlusion import detect_occlusion
     d = golden("occlusion.npz")
