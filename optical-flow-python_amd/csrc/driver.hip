@@ -236,6 +236,7 @@ struct of_ctx {
   size_t sor_ring_cap = 0;  // bytes
   int sor_fallbacks = 0;    // pipelined solves rerun per sweep (hand-off timeout)
   float *d_gather = nullptr;  // rank 0's RCCL gather receive buffer (grow-only)
+  hipStream_t gstream = nullptr;  // the gather's own stream (of_rccl_gather_slots)
   size_t gather_cap = 0;
   // of_set_progress: display / per-stage report callback (never on batch lanes)
   of_progress_fn prog_fn = nullptr;
@@ -2106,6 +2107,10 @@ int of_ctx_destroy(of_ctx *c) {
   if (c->d_sorp) hipFree(c->d_sorp);
   if (c->d_sor_ring) hipFree(c->d_sor_ring);
   if (c->d_gather) hipFree(c->d_gather);
+  if (c->gstream) {
+    hipStreamSynchronize(c->gstream);
+    hipStreamDestroy(c->gstream);
+  }
   hipFree(c->d_rpart);
   hipFree(c->d_rlog);
   hipFree(c->d_mm);
@@ -3112,9 +3117,18 @@ int of_rccl_gather_flows(of_ctx *c, int nslots, float *out_uv_rank0) {
   return of_rccl_gather_slots(c, 0, nslots, out_uv_rank0);
 }
 
+// May run while a pair stream is open on this context, whose lane 0 is the
+// context itself (bench.py gathers step s's slots while step s + 1 computes):
+// so no API_BEGIN / API_END here -- they reset the context's arena and drain
+// its pending solves under the lane thread -- and the gather's copies and
+// RCCL calls go to a stream of its own (the slots' flows are complete: a
+// ticket is done only after its lane's stream reached the end of the pair).
 int of_rccl_gather_slots(of_ctx *c, int first, int nslots, float *out_uv_rank0) {
-  API_BEGIN(c)
+  if (!c) return OF_EINVAL;
+  try {
+  HIPCHK(hipSetDevice(c->device));
   REQUIRE(c->comm, OF_EINVAL, "of_rccl_init first");
+  if (!c->gstream) create_stream(&c->gstream);
   REQUIRE(first >= 0 && nslots >= 1 && first + nslots <= (int)c->slots.size(), OF_EINVAL, "bad slot range");
   Slot *sl = c->slots.data() + first;
   const int H = sl[0].H, W = sl[0].W;
@@ -3137,14 +3151,14 @@ int of_rccl_gather_slots(of_ctx *c, int first, int nslots, float *out_uv_rank0) 
   // ncclGroupStart and ncclGroupEnd, so a failed copy cannot leave a group open
   if (c->rank == 0)
     for (int s = 0; s < nslots; ++s)
-      HIPCHK(hipMemcpyAsync(recv + per * s, sl[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(recv + per * s, sl[s].uv, sizeof(float) * per, hipMemcpyDeviceToDevice, c->gstream));
   ncclResult_t r = ncclGroupStart();
   for (int s = 0; s < nslots && r == ncclSuccess; ++s) {
     if (c->rank == 0) {
       for (int src = 1; src < c->nranks && r == ncclSuccess; ++src)
-        r = ncclRecv(recv + per * ((size_t)src * nslots + s), per, ncclFloat, src, c->comm, c->stream);
+        r = ncclRecv(recv + per * ((size_t)src * nslots + s), per, ncclFloat, src, c->comm, c->gstream);
     } else {
-      r = ncclSend(sl[s].uv, per, ncclFloat, 0, c->comm, c->stream);
+      r = ncclSend(sl[s].uv, per, ncclFloat, 0, c->comm, c->gstream);
     }
   }
   ncclResult_t r2 = ncclGroupEnd();
@@ -3152,9 +3166,14 @@ int of_rccl_gather_slots(of_ctx *c, int first, int nslots, float *out_uv_rank0) 
           std::string("rccl gather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   if (c->rank == 0 && out_uv_rank0)
     HIPCHK(hipMemcpyAsync(out_uv_rank0, recv, sizeof(float) * per * nslots * c->nranks, hipMemcpyDeviceToHost,
-                          c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  API_END(c)
+                          c->gstream));
+  HIPCHK(hipStreamSynchronize(c->gstream));
+  return OF_OK;
+  } catch (const OfError &e) {
+    return fail(c, e);
+  } catch (const std::exception &e) {
+    return fail(c, OfError{OF_ENOMEM, e.what()});
+  }
 }
 
 int of_rccl_finalize(of_ctx *c) {

@@ -179,6 +179,67 @@ def test_rccl_gather_single_rank():
         ctx.close()
 
 
+def test_rccl_gather_while_pool_computes():
+    """bench.py's N > 1 pattern: step s's slots are gathered with RCCL while
+    step s + 1 computes on the pool, whose lane 0 is the context itself.  The
+    gather must not touch the context's arena, stream or pending solves (it
+    runs on a stream of its own): every slot's flow, gathered or computed
+    meanwhile, equals of_pairs_run's bitwise (single-rank communicator)."""
+    from optical_flow import _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    lib = ctx.lib
+    H, W, n, lanes = 120, 160, 3, 3
+    frames = [synth_pair(H, W, 60 + s)[:2] for s in range(n)]
+
+    def upload():
+        for k in range(2):
+            for s, (a, b) in enumerate(frames):
+                ctx.check(lib.of_pair_upload(ctx.handle, k * n + s, _native.ptr(_native.f32(a)),
+                                             _native.ptr(_native.f32(b)), H, W, 3))
+    upload()
+    P0 = _params("classic+nl-fast")
+    ctx.check(lib.of_pairs_run(ctx.handle, n, C.byref(P0), lanes, None))
+    ref = np.empty((n, 2, H, W), np.float32)
+    for s in range(n):
+        ctx.check(lib.of_pair_download(ctx.handle, s, _native.ptr(ref[s])))
+    upload()
+    uid = C.create_string_buffer(128)
+    ctx.check(lib.of_rccl_unique_id(uid))
+    ctx.check(lib.of_rccl_init(ctx.handle, uid.raw, 1, 0))
+    sets = [(C.c_int * n)(*range(k * n, (k + 1) * n)) for k in range(2)]
+    gathered = []
+    try:
+        ctx.check(lib.of_pairs_open(ctx.handle, H, W, 3, C.byref(P0), lanes))
+        try:
+            first = []
+            for step in range(4):
+                t = C.c_int64(0)
+                ctx.check(lib.of_pairs_submit_slots(ctx.handle, n, sets[step % 2], C.byref(t)))
+                first.append(t.value)
+                if step:
+                    prev = step - 1
+                    for tk in range(first[prev], first[prev] + n):
+                        ctx.check(lib.of_pairs_wait(ctx.handle, tk))
+                    out = np.full((n, 2, H, W), np.nan, np.float32)
+                    ctx.check(lib.of_rccl_gather_slots(ctx.handle, (prev % 2) * n, n, _native.ptr(out)))
+                    gathered.append(out)
+            for tk in range(first[3], first[3] + n):
+                ctx.check(lib.of_pairs_wait(ctx.handle, tk))
+        finally:
+            ctx.check(lib.of_pairs_close(ctx.handle))
+        for out in gathered:
+            np.testing.assert_array_equal(out, ref)
+        for k in range(2):
+            for s in range(n):
+                uv = np.empty((2, H, W), np.float32)
+                ctx.check(lib.of_pair_download(ctx.handle, k * n + s, _native.ptr(uv)))
+                np.testing.assert_array_equal(uv, ref[s])
+    finally:
+        lib.of_rccl_finalize(ctx.handle)
+        ctx.close()
+
+
 @pytest.mark.parametrize("lanes,n,H,W", [(1, 3, 60, 88), (2, 5, 60, 88), (3, 4, 270, 480), (3, 3, 540, 960)])
 def test_pairs_run_host_matches_estimate_flow(lanes, n, H, W):
     """of_pairs_run_host (uint8 frames in host memory -> flows in host
