@@ -2005,8 +2005,12 @@ void stage_free(of_ctx *l);
 
 }  // namespace
 
+// Entries that compute on the context refuse while a pair stream is open on
+// it: the pool's lane 0 is the context itself, and these reset its arena and
+// drain its pending solves (before the try: the error path clears them too)
 #define API_BEGIN(ctx)            \
   if (!ctx) return OF_EINVAL;     \
+  if (ctx->pool) return fail(ctx, OfError{OF_EINVAL, "a pair stream is open on this context (of_pairs_close first)"}); \
   try {                           \
     HIPCHK(hipSetDevice(ctx->device)); \
     ctx->arena.reset();            \
@@ -2027,6 +2031,29 @@ void stage_free(of_ctx *l);
   }                                          \
   catch (const std::exception &e) {          \
     return fail(ctx, OfError{OF_ENOMEM, e.what()}); \
+  }
+
+// Slot copies (of_pair_upload / of_pair_download) may run while the pair
+// pool computes on the context: no arena, no pending solves, and a stream of
+// their own when a pool is open (the gather's)
+hipStream_t io_stream(of_ctx *c) {
+  if (!c->pool) return c->stream;
+  if (!c->gstream) create_stream(&c->gstream);
+  return c->gstream;
+}
+#define API_BEGIN_IO(ctx)               \
+  if (!ctx) return OF_EINVAL;           \
+  try {                                 \
+    HIPCHK(hipSetDevice(ctx->device));  \
+    hipStream_t ios = io_stream(ctx);
+#define API_END_IO(ctx)                                 \
+  return OF_OK;                                         \
+  }                                                     \
+  catch (const OfError &e) {                            \
+    return fail(ctx, e);                                \
+  }                                                     \
+  catch (const std::exception &e) {                     \
+    return fail(ctx, OfError{OF_ENOMEM, e.what()});     \
   }
 
 extern "C" {
@@ -2386,7 +2413,7 @@ int of_alt_ba_flow_base(of_ctx *c, of_params *P, const float *images, int H, int
 
 // ---- device-resident slots ----
 int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int H, int W, int C) {
-  API_BEGIN(c)
+  API_BEGIN_IO(c)
   REQUIRE(slot >= 0 && slot < 4096 && im1 && im2 && (C == 1 || C == 3), OF_EINVAL, "bad arguments");
   if ((int)c->slots.size() <= slot) c->slots.resize(slot + 1);
   Slot &s = c->slots[slot];
@@ -2407,10 +2434,10 @@ int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int 
   s.W = W;
   s.C = C;
   s.u8 = false;
-  HIPCHK(hipMemcpyAsync(s.rgb1, im1, n, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(s.rgb2, im2, n, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  API_END(c)
+  HIPCHK(hipMemcpyAsync(s.rgb1, im1, n, hipMemcpyHostToDevice, ios));
+  HIPCHK(hipMemcpyAsync(s.rgb2, im2, n, hipMemcpyHostToDevice, ios));
+  HIPCHK(hipStreamSynchronize(ios));
+  API_END_IO(c)
 }
 
 int of_pair_run(of_ctx *c, int slot, of_params *P, of_stats *st) {
@@ -3083,12 +3110,12 @@ int of_pairs_close(of_ctx *c) {
 }
 
 int of_pair_download(of_ctx *c, int slot, float *out_uv) {
-  API_BEGIN(c)
+  API_BEGIN_IO(c)
   REQUIRE(slot >= 0 && slot < (int)c->slots.size() && c->slots[slot].uv && out_uv, OF_EINVAL, "bad slot");
   Slot &s = c->slots[slot];
-  HIPCHK(hipMemcpyAsync(out_uv, s.uv, sizeof(float) * 2 * (size_t)s.H * s.W, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  API_END(c)
+  HIPCHK(hipMemcpyAsync(out_uv, s.uv, sizeof(float) * 2 * (size_t)s.H * s.W, hipMemcpyDeviceToHost, ios));
+  HIPCHK(hipStreamSynchronize(ios));
+  API_END_IO(c)
 }
 
 // ---- RCCL gather: one process per GPU ----

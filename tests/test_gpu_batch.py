@@ -184,7 +184,9 @@ def test_rccl_gather_while_pool_computes():
     step s + 1 computes on the pool, whose lane 0 is the context itself.  The
     gather must not touch the context's arena, stream or pending solves (it
     runs on a stream of its own): every slot's flow, gathered or computed
-    meanwhile, equals of_pairs_run's bitwise (single-rank communicator)."""
+    meanwhile, equals of_pairs_run's bitwise (single-rank communicator).
+    Slot downloads work meanwhile; entries that compute on the context are
+    refused (ValueError) instead of resetting lane 0's arena."""
     from optical_flow import _native
     from optical_flow.utils.synthetic import synth_pair
     ctx = _native.Context(0)
@@ -224,6 +226,12 @@ def test_rccl_gather_while_pool_computes():
                     out = np.full((n, 2, H, W), np.nan, np.float32)
                     ctx.check(lib.of_rccl_gather_slots(ctx.handle, (prev % 2) * n, n, _native.ptr(out)))
                     gathered.append(out)
+                    # slot copies are pool-safe too; compute entries refuse
+                    uv = np.empty((2, H, W), np.float32)
+                    ctx.check(lib.of_pair_download(ctx.handle, (prev % 2) * n + 1, _native.ptr(uv)))
+                    np.testing.assert_array_equal(uv, ref[1])
+                    with pytest.raises(ValueError):
+                        ctx.check(lib.of_pair_run(ctx.handle, 0, C.byref(P0), None))
             for tk in range(first[3], first[3] + n):
                 ctx.check(lib.of_pairs_wait(ctx.handle, tk))
         finally:
