@@ -152,12 +152,18 @@ __global__ __launch_bounds__(256) void k_rof_iters(const float *__restrict__ im,
                                                    float2 *__restrict__ pout, int H, int W, int P, size_t ps,
                                                    float theta, float delta, int iters) {
   __shared__ float s_py[4][64], s_u[4][64];  // wave-boundary rows: p_y of the last, u of the first
-  im += blockIdx.z * ps;
-  pin += blockIdx.z * ps;
-  pout += blockIdx.z * ps;
+  // XCD-aware tile order (common.h: of_xcd_tile): each XCD a contiguous run
+  // of the (frame, row, column) tiles, so the 8-pixel halos two neighbouring
+  // tiles both read meet in one L2 instead of being fetched twice
+  const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
+  const int t = of_xcd_tile(blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
+  const int bz = t / gxy, by = (t - bz * gxy) / gx, bx = t - bz * gxy - by * gx;
+  im += bz * ps;
+  pin += bz * ps;
+  pout += bz * ps;
   const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
-  const int gj = blockIdx.x * ROF_TW - ROF_K + lane;
-  const int gr0 = blockIdx.y * ROF_TH - ROF_K + w * ROF_RPW;  // image row of the wave's first row
+  const int gj = bx * ROF_TW - ROF_K + lane;
+  const int gr0 = by * ROF_TH - ROF_K + w * ROF_RPW;  // image row of the wave's first row
   const bool colin = (unsigned)gj < (unsigned)W, left = gj > 0, right = gj < W - 1;
   float I[ROF_RPW], U[ROF_RPW];
   float2 Q[ROF_RPW];
