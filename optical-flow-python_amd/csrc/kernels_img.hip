@@ -217,7 +217,7 @@ __global__ void k_rof_final(const float *__restrict__ im, const float2 *__restri
   im += blockIdx.z * ps;
   p += blockIdx.z * ps;
   out += blockIdx.z * ps;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     size_t k = (size_t)i * P + j;
     out[k] = im[k] - alp * (im[k] + theta * rof_div(p, i, j, P));
@@ -231,7 +231,7 @@ __global__ void k_correlate(const float *__restrict__ in, float *__restrict__ ou
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
   const int ch = t.kh / 2, cw = t.kw / 2;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     float s = 0.0f;
     for (int a = 0; a < t.kh; ++a) {
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_correlate_k(const float *__res
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
   constexpr int ch = KH / 2, cw = KW / 2;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     int cols[KW];
 #pragma unroll
@@ -310,7 +310,7 @@ __global__ void k_bspline_rows(const float *__restrict__ in, float *__restrict__
                                BsplTaps t) {
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     const float *row = in + (size_t)i * P;
     float s = t.h[0] * row[j];
@@ -322,7 +322,7 @@ __global__ void k_bspline_cols(const float *__restrict__ in, float *__restrict__
                                BsplTaps t) {
   in += blockIdx.z * ps;
   out += blockIdx.z * ps;
-  OF_FOR_PIXELS(H, W) {
+  OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
     float s = t.h[0] * in[(size_t)i * P + j];
     for (int k = 1; k <= OF_BSPL_K; ++k)
