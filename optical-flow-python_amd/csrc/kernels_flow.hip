@@ -755,10 +755,18 @@ struct Bitonic {
           kb[r] = take_min ? bn : bx;
         }
       } else {
+        // every partner first, then the minima: the DPP moves of a key are
+        // not right behind the v_xor that wrote it (VALU -> DPP hazard nops)
+        uint64_t pa[NPER], pb[NPER];
 #pragma unroll
         for (int r = 0; r < NPER; ++r) {
-          ka[r] = wmf_min_neg(ka[r], xor_lane64(ka[r], lj));
-          kb[r] = wmf_min_neg(kb[r], xor_lane64(kb[r], lj));
+          pa[r] = xor_lane64(ka[r], lj);
+          pb[r] = xor_lane64(kb[r], lj);
+        }
+#pragma unroll
+        for (int r = 0; r < NPER; ++r) {
+          ka[r] = wmf_min_neg(ka[r], pa[r]);
+          kb[r] = wmf_min_neg(kb[r], pb[r]);
         }
       }
     } else {
