@@ -685,7 +685,11 @@ __device__ __forceinline__ uint64_t wmf_key(float v, unsigned pos) {
   const double f = __builtin_isnan(v) ? 0x1p1001 : (__builtin_isinf(v) ? e : d);
   return __builtin_bit_cast(uint64_t, f) | (uint64_t)pos;
 }
-#define WMF_PAD_KEY (__builtin_bit_cast(uint64_t, 0x1p1002) | 0xffffull)
+// padding keys: above every value; position (RW, 0), one row below the
+// region -- out of every lane's window (dy = RW - py > 2 hsz), yet its
+// record address (RW * RP) is inside the LDS allocation, so the chunk walk
+// reads it without a select
+#define WMF_PAD_KEY(RW) (__builtin_bit_cast(uint64_t, 0x1p1002) | ((uint64_t)(RW) << 8))
 __device__ __forceinline__ double wmf_d(uint64_t k) { return __builtin_bit_cast(double, k); }
 // v_min_f64 / v_max_f64 without the canonicalising v_max_f64 x, x that the
 // builtins add in IEEE mode (keys are never NaN, and fp64 denormals -- the
@@ -902,8 +906,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     // compiler sink the last sample's read into a branch behind the others
     const uint64_t pm = 0ull - (uint64_t)(lane * NPER + r >= nreg);
     const uint64_t ka = wmf_key(rv[r].x, rpos[r]), kb = wmf_key(rv[r].y, rpos[r]);
-    a[r] = ka ^ ((ka ^ WMF_PAD_KEY) & pm);
-    b[r] = kb ^ ((kb ^ WMF_PAD_KEY) & pm);
+    a[r] = ka ^ ((ka ^ WMF_PAD_KEY(RW)) & pm);
+    b[r] = kb ^ ((kb ^ WMF_PAD_KEY(RW)) & pm);
     smp[(rpos[r] >> 8) * RP + (rpos[r] & 0xffu)] = WmfRec<GC>::make(rg[r][0], rg[r][1], rg[r][2], ro[r]);
   }
   wmf_sum_t *cs = csum + lane;
@@ -915,11 +919,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   for (int r = 0; r < NPER; ++r) {
     const int e = lane * NPER + r;
     const unsigned pa = (uint16_t)a[r], pb = (uint16_t)b[r];
-    ku[e] = (uint16_t)pa;  // padding keys -> 0xffff: out of every window
+    ku[e] = (uint16_t)pa;  // padding keys -> (RW, 0): out of every window
     kv[e] = (uint16_t)pb;
     const int qa = (pa >> 8) * RP + (pa & 0xffu), qb_ = (pb >> 8) * RP + (pb & 0xffu);
-    if (pa != 0xffffu) cid[WMF_CID_PAIR ? 2 * qa : qa] = (uint8_t)(e / CH);
-    if (pb != 0xffffu) cid[WMF_CID_PAIR ? 2 * qb_ + 1 : RW * RP + qb_] = (uint8_t)(e / CH);
+    const unsigned padpos = (unsigned)RW << 8;
+    if (pa != padpos) cid[WMF_CID_PAIR ? 2 * qa : qa] = (uint8_t)(e / CH);
+    if (pb != padpos) cid[WMF_CID_PAIR ? 2 * qb_ + 1 : RW * RP + qb_] = (uint8_t)(e / CH);
   }
   __syncthreads();
   WMF_STAMP(2);
@@ -1004,7 +1009,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // the crossing chunks' sorted positions (ry << 8 | rx), 8 per 16-B read;
   // window offsets straight from the position bytes (dy = ry - py and
   // dx = rx - px as unsigned: out of the window unless both <= span; padding
-  // keys have ry = 255)
+  // keys have ry = RW)
   const uint4 *wu = reinterpret_cast<const uint4 *>(ku + chu * CH), *wv = reinterpret_cast<const uint4 *>(kv + chv * CH);
   for (int g = 0; g < CH / 8; ++g) {
     const uint4 A = wu[g], B = wv[g];
@@ -1020,8 +1025,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       const unsigned dyb = ((wb >> (sh + 8)) & 0xffu) - (unsigned)py, dxb = ((wb >> sh) & 0xffu) - (unsigned)px;
       ina[i] = max(dya, dxa) <= span;
       inb[i] = max(dyb, dxb) <= span;
-      qa[i] = ina[i] ? dya * (unsigned)RP + dxa : 0u;
-      qv[i] = inb[i] ? dyb * (unsigned)RP + dxb : 0u;
+      // qb + qa = ry * RP + rx: inside the region for every real sample, the
+      // word after it for a padding key (no select needed for the read)
+      qa[i] = dya * (unsigned)RP + dxa;
+      qv[i] = dyb * (unsigned)RP + dxb;
       ra[i] = smp[qb + qa[i]];
       rb[i] = smp[qb + qv[i]];
     }
