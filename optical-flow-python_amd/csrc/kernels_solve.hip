@@ -58,7 +58,7 @@ __device__ __forceinline__ void prologue_sum(double (&out)[NV], const double *__
 
 // per-block partials -> part[v * PCG_MAX_BLOCKS + bid] (plain stores)
 template <int NV>
-__device__ __forceinline__ void write_partials(double (&v)[NV], double *part, double *lds) {
+__device__ __forceinline__ void write_partials(double (&v)[NV], double *part, double *lds, int slot = -1) {
   const int tid = threadIdx.x + threadIdx.y * blockDim.x, nt = blockDim.x * blockDim.y;
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
@@ -67,7 +67,7 @@ __device__ __forceinline__ void write_partials(double (&v)[NV], double *part, do
     for (int k = 0; k < NV; ++k) lds[k * 8 + (tid >> 6)] = v[k];
   __syncthreads();
   if (tid == 0) {
-    const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+    const int bid = slot >= 0 ? slot : blockIdx.x + blockIdx.y * gridDim.x;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       double s = 0.0;
@@ -367,9 +367,14 @@ __global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands)
   const __amdgpu_buffer_rsrc_t rro = cg_rsrc(g.r_out, vbytes);
   const __amdgpu_buffer_rsrc_t rpn = cg_rsrc(g.p_new, vbytes);
   const unsigned ps4 = (unsigned)(g.ps * 4);
+  // XCD-aware tile order (common.h): neighbouring strips / band groups share
+  // their halo rows in one L2.  The partials slot is the tile, so the
+  // fixed-order sums (and the iterates) do not depend on the order
+  const int tile = of_xcd_tile(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int tby = tile / (int)gridDim.x, tbx = tile - tby * (int)gridDim.x;
   // threadIdx.y is wave-uniform (64 x 4 blocks): make every row index scalar
-  const int lane = threadIdx.x, band = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.y);
-  const int jc = blockIdx.x * PCG_SW - 2 + 2 * lane;
+  const int lane = threadIdx.x, band = tby * 4 + __builtin_amdgcn_readfirstlane(threadIdx.y);
+  const int jc = tbx * PCG_SW - 2 + 2 * lane;
   const bool ok0 = jc >= 0 && jc < W, ok1 = jc + 1 < W && jc >= 0;
   const bool out_lane = lane >= 1 && lane <= 62;
   const unsigned off4 = ok0 ? (unsigned)jc * 4u : CG_OOB, off8 = ok0 ? (unsigned)jc * 8u : CG_OOB;
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(256) void k_cg(PcgArgs g, int k, int R, int nbands)
       }
     }
   }
-  write_partials<5>(acc, g.part_wr, lds);
+  write_partials<5>(acc, g.part_wr, lds, tile);
 }
 
 // ---------------------------------------------------------------------------
