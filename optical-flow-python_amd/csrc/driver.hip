@@ -869,7 +869,7 @@ void cheb_poly(int m, double a, double b, double *cB) {
 
 // Launch geometry of the fused CG iteration kernels for an H x W level.
 // k_cg ('pcg'): strips of PCG_SW columns x bands of R rows, 4 bands (waves)
-// per 256-thread block, ~CG_PCG_WAVES (512) waves per launch.  k_cgs ('backslash'): strips
+// per 256-thread block, ~CG_PCG_WAVES (640) waves per launch.  k_cgs ('backslash'): strips
 // of PCG_SWP columns x bands of R rows, one band per block, ~512 blocks (2
 // per CU).  Every block writes one slot of the partials buffer, so the grid
 // may not exceed PCG_MAX_BLOCKS blocks: levels wider than PCG_MAX_BLOCKS
@@ -909,9 +909,11 @@ void cheb_poly(int m, double a, double b, double *cB) {
 // k_cg waves per launch: config 3 (Classic-C + 'pcg', 720p, 4 lanes) 8.5 /
 // 9.45 / 9.73 / 9.42 / 8.10 / 7.40 pairs/s at 256 / 384 / 512 / 768 / 1536 /
 // 2048 (profiles/r5au_pcg_waves_ab.log, r5av_pcg_waves_ab.log): shorter
-// bands lose to their halo rows and to the lanes' shared CUs
+// bands lose to their halo rows and to the lanes' shared CUs; with the
+// XCD-aware tile order 10.43 / 10.57 / 10.32 at 512 / 640 / 768
+// (profiles/r5ba_pcg_waves_xcd_ab.log)
 #ifndef CG_PCG_WAVES
-#define CG_PCG_WAVES 512
+#define CG_PCG_WAVES 640
 #endif
 int cg_geometry(int H, int W, bool split, of_cg_geometry *g, int target_blocks = CGS_TARGET_BLOCKS) {
   if (H < 1 || W < 1) return OF_EINVAL;
