@@ -4,7 +4,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--lanes L]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One process per GPU.  A step = every rank runs estimate_flow on its P
+One process per GPU.  `--gpus N` with N > 1 and no launcher around it
+(WORLD_SIZE unset) starts `python -m torch.distributed.run --nproc-per-node N
+bench.py <same arguments>` as a child process before anything touches the GPU,
+relays rank 0's JSON line and exits with the child's status; under a launcher
+WORLD_SIZE must equal --gpus.  `--rccl-self` (N = 1) runs the timed loop with
+a one-rank RCCL communicator and the per-step gather: the one-GPU proxy of the
+N > 1 timed path.  A step = every rank runs estimate_flow on its P
 pairs (default 8 = config 5's 64 pairs over 8 GPUs) with the frames already
 resident in HBM (uploaded to device slots before the timed region) and the
 flows left there (RGB -> gray/Lab, ROF, pyramids, GNC x levels x IRLS, L
@@ -47,9 +53,19 @@ sys.path.insert(0, os.path.join(ROOT, "optical-flow-python_amd"))
 
 import numpy as np  # noqa: E402
 
-from optical_flow import _abi, _native  # noqa: E402  (loads liboptflow.so before torch)
-from optical_flow.methods.config import load_of_method  # noqa: E402
 from optical_flow.utils.synthetic import synth_pair  # noqa: E402
+
+# the library (liboptflow.so, loaded before torch) and the method registry are
+# imported in main() once the launch decision is made: a process that spawns
+# the ranks never touches the GPU (import_native)
+_abi = _native = load_of_method = None
+
+
+def import_native():
+    global _abi, _native, load_of_method
+    from optical_flow import _abi as a, _native as n
+    from optical_flow.methods.config import load_of_method as lm
+    _abi, _native, load_of_method = a, n, lm
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -80,7 +96,7 @@ VALU_ISSUE_PEAK = 256 * 4 * 0.5 * CLOCK_HZ
 WMF_CENSUS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5_wmf_census.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -95,7 +111,60 @@ def parse():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-stream", action="store_true", help="skip the streamed (pair pool) rate")
     ap.add_argument("--cpu-sample", type=int, default=360, help="crop height of the CPU-baseline sample")
-    return ap.parse_args()
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="N = 1: one-rank RCCL communicator + the per-step gather in the timed loop "
+                         "(the one-GPU proxy of the N > 1 timed path)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rendezvous only (no library, no GPU): rank 0 prints the line's "
+                         "n_gpus and the ranks seen (the CPU test of the --gpus N launch)")
+    return ap.parse_args(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv):
+    """--gpus N > 1 with no launcher around bench.py: run `python -m
+    torch.distributed.run --nproc-per-node N bench.py <argv>` as a child (the
+    contract's N-rank launch; never an exec from this process), pass its
+    stderr and non-JSON stdout through, print rank 0's JSON line once with
+    the launch recorded in it, and return the child's exit status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    line = None
+    for out in proc.stdout:
+        if out.startswith('{"metric"'):
+            line = out
+        else:
+            sys.stderr.write(out)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line is not None:
+        rec = json.loads(line)
+        rec["launch"] = (f"bench.py --gpus {args.gpus}: torch.distributed.run child, "
+                         f"{args.gpus} processes (one per GPU), rc {rc}")
+        print(json.dumps(rec), flush=True)
+    elif rc == 0:
+        sys.stderr.write("bench.py: the ranks exited without a result line\n")
+        rc = 1
+    return rc
+
+
+def launch_check(args):
+    """WORLD_SIZE from a launcher must match --gpus (a mismatch would time a
+    different job than the one asked for)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}\n")
+        return 2
+    return 0
 
 
 def dist_setup(args):
@@ -456,11 +525,43 @@ def metric_name(args):
     return f"image-pairs/sec at {args.width}x{args.height} {tag}{solver} (+ ms/pyramid-level, AEPE)"
 
 
-def main():
-    args = parse()
+def dry_run(args, dist, world, rank, local):
+    """The launch and rendezvous of an N-rank run without the library: every
+    rank reports (rank, local rank, world); rank 0 prints the line."""
+    seen = [None] * world
+    if dist is not None:
+        dist.all_gather_object(seen, [rank, local, world])
+    else:
+        seen = [[rank, local, world]]
+    barrier(dist)
+    t = max_over_ranks(dist, 0.001 * (1 + rank))
+    if rank == 0:
+        print(json.dumps({"metric": metric_name(args), "value": None, "unit": "pairs/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True, "ranks": seen,
+                          "max_over_ranks": t, "rccl_nranks": None}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = launch_check(args)
+    if rc:
+        return rc
+    if args.gpus > 1 and os.environ.get("WORLD_SIZE") is None:
+        return spawn_ranks(args, argv)
+    if args.rccl_self and args.gpus != 1:
+        sys.stderr.write("bench.py: --rccl-self is the N = 1 proxy\n")
+        return 2
     global WORKLOAD
     WORKLOAD = workload_key(args)
     dist, world, rank, local = dist_setup(args)
+    if args.dry_run:
+        dry_run(args, dist, world, rank, local)
+        return 0
+    import_native()
     ctx = _native.Context(local)
     lib = ctx.lib
     H, W = args.height, args.width
@@ -480,13 +581,21 @@ def main():
     p1 = (vp * args.pairs)(*[x.ctypes.data for x in f1])
     p2 = (vp * args.pairs)(*[x.ctypes.data for x in f2])
     po = (vp * args.pairs)(*[o.ctypes.data for o in outs])
-    if world > 1:
+    # the RCCL communicator: N ranks, or one rank for the --rccl-self proxy
+    gathering = world > 1 or args.rccl_self
+    if gathering:
         uid = C.create_string_buffer(128)
         if rank == 0:
             ctx.check(lib.of_rccl_unique_id(uid))
         obj = [bytes(uid.raw)]
-        dist.broadcast_object_list(obj, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(obj, src=0)
         ctx.check(lib.of_rccl_init(ctx.handle, obj[0], world, rank))
+    nr = C.c_int64(0)
+    ctx.check(lib.of_get_option(ctx.handle, _abi.OF_OPT_RCCL_NRANKS, C.byref(nr)))
+    rccl_nranks = int(nr.value)
+    if gathering and rccl_nranks != world:
+        raise RuntimeError(f"RCCL communicator has {rccl_nranks} ranks, expected {world}")
 
     # the timed steps: frames resident in HBM (two sets of device slots,
     # uploaded here, outside the timed region), flows left in HBM (+ the RCCL
@@ -510,7 +619,7 @@ def main():
     def pwait(s, t0_):
         for t in range(t0_, t0_ + NP):
             ctx.check(lib.of_pairs_wait(ctx.handle, t))
-        if world > 1:
+        if gathering:
             ctx.check(lib.of_rccl_gather_slots(ctx.handle, (s % 2) * NP, NP, None))
 
     def pool_steps(k):
@@ -538,7 +647,7 @@ def main():
     # the same steps as one of_pairs_run call each (lanes drain at step end)
     def step():
         run_step(ctx, P0, NP, args.lanes)
-        if world > 1:
+        if gathering:
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, NP, None))
     step()
     barrier(dist)
@@ -556,7 +665,7 @@ def main():
     # host memory, copies overlapped inside the library
     def hstep():
         ctx.check(lib.of_pairs_run_host(ctx.handle, args.pairs, p1, p2, H, W, 3, C.byref(P0), args.lanes, po, None))
-        if world > 1:
+        if gathering:
             ctx.check(lib.of_rccl_gather_flows(ctx.handle, args.pairs, None))
     hsteps = args.steps
     hstep()  # warm-up (pinned staging buffers)
@@ -677,10 +786,16 @@ def main():
                        "method": args.method, "height": H, "width": W, "pairs_per_gpu": args.pairs,
                        "lanes": min(args.lanes, args.pairs),
                        "solver": args.solver or "backslash (GPU block-Jacobi PCG surrogate)",
-                       "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"},
+                       "parallelism": f"pairs sharded 1/GPU x {world}, RCCL gather"
+                                      + (" (one-rank proxy, --rccl-self)" if args.rccl_self else "")},
+            "rccl_nranks": rccl_nranks if gathering else None,
+            "rccl_gather_per_step": bool(gathering),
             "timed_region": "frames resident in HBM (device slots, uploaded before the timed region) -> "
                             "flows (fp32) left in HBM; K steps queued back to back through the pair pool "
-                            "(of_pairs_submit_slots)",
+                            "(of_pairs_submit_slots), each step's flows gathered to rank 0 over RCCL when "
+                            "rccl_gather_per_step (N > 1, or --rccl-self); round 5 on: the steps overlap (before "
+                            "round 5 each step drained its lanes -- compare those rounds with "
+                            "device_resident_drained)",
             "device_resident_drained": {"value": round(world * NP * args.steps / d_elapsed, 4),
                                         "ms_per_step": round(1e3 * d_elapsed / args.steps, 3),
                                         "steps": args.steps,
@@ -714,11 +829,13 @@ def main():
             "kernel_ms_per_pair_concurrent": kms(ktimes, args.pairs),
         }
         print(json.dumps(line), flush=True)
-    if dist is not None:
+    if gathering:
         lib.of_rccl_finalize(ctx.handle)
+    if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

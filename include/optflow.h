@@ -188,6 +188,9 @@ int of_set_option(of_ctx *ctx, int option, int value);
  *                         grow-only buffers (arena, SOR sweep ring, gather
  *                         buffer): flat across repeated pairs of one size */
 #define OF_OPT_DEVICE_BYTES 4
+/*   OF_OPT_RCCL_NRANKS    ranks of the context's RCCL communicator as RCCL
+ *                         reports them (ncclCommCount; 0 before of_rccl_init) */
+#define OF_OPT_RCCL_NRANKS 5
 int of_get_option(of_ctx *ctx, int option, int64_t *value);
 /* progress of compute_flow / compute_flow_base: the reference's `display`
  * prints and its per-GNC-stage report (classic_nl.py:141-196, 255-256;
@@ -303,7 +306,10 @@ int of_pairs_run_host(of_ctx *ctx, int npairs, const uint8_t *const *im1, const 
  *   of_pairs_wait   block until that pair's flow is in its out_uv
  *   of_pairs_close  finish the queued pairs, stop and free the pool
  * Flows equal of_pairs_run_host's with the same `lanes` bitwise.  While a
- * stream is open, of_pairs_run / of_pairs_run_host refuse the context.
+ * stream is open the context's compute entries (of_pairs_run,
+ * of_pairs_run_host, the stage entries ...) and its settings and profiling
+ * calls (of_set_option, of_set_profiling, of_set_solve_log, of_kernel_times,
+ * of_kernel_timeline) return OF_EINVAL: lane 0 of the pool is the context.
  */
 int of_pairs_open(of_ctx *ctx, int H, int W, int C, const of_params *params, int lanes);
 int of_pairs_submit(of_ctx *ctx, int n, const uint8_t *const *im1, const uint8_t *const *im2, float *const *out_uv,
@@ -312,8 +318,9 @@ int of_pairs_wait(of_ctx *ctx, int64_t ticket);
 int of_pairs_close(of_ctx *ctx);
 /* the same pool over device-resident pairs: queue the pairs of n slots of
  * this context (of_pair_upload; frame size = the stream's); each flow stays
- * in its slot (of_pair_download, of_rccl_gather_slots).  A slot must not be
- * submitted again or re-uploaded before its ticket is waited for.  Tickets
+ * in its slot (of_pair_download, of_rccl_gather_slots).  A slot queued and
+ * not yet finished is refused by of_pairs_submit_slots, of_pair_upload and
+ * of_pair_download (OF_EINVAL) until its ticket is done.  Tickets
  * share the host submissions' sequence; flows equal of_pairs_run's with the
  * same `lanes` bitwise (the bench's HBM-resident rate: consecutive batches
  * queued back to back, so the lanes never drain between them). */
@@ -418,6 +425,14 @@ int of_detect_occlusion(of_ctx *ctx, const float *uv, const float *images, int H
 /* denoise_color_weighted_medfilt2 (utils/weighted_median.py:24-112) */
 int of_weighted_median(of_ctx *ctx, const float *uv, const float *guide, int gc, const float *occ,
                        int H, int W, int area_hsz, double sigma_i, float *out);
+/* flow_to_color (viz/flow_color.py:77-107): Middlebury colour coding of an
+ * interleaved (H, W, 2) flow of dtype 0 = float32 or 1 = float64 into an
+ * (H, W, 3) uint8 image; |u| or |v| > 1e9 is unknown (black).  has_max = 0
+ * normalises by the largest known radius, else by max(max_flow, 1e-8).  The
+ * arithmetic keeps numpy's dtype rules (the flow's dtype up to the wheel
+ * position, float64 for the colour blend) */
+int of_flow_to_color(of_ctx *ctx, const void *flow, int dtype, int H, int W, int has_max, double max_flow,
+                     uint8_t *out_rgb);
 /* scipy.ndimage.median_filter(size, mode='reflect') on each of `planes` planes */
 int of_median_filter(of_ctx *ctx, const float *in, int H, int W, int planes, int size, float *out);
 

@@ -2045,11 +2045,14 @@ void stage_free(of_ctx *l);
 // Slot copies (of_pair_upload / of_pair_download) may run while the pair
 // pool computes on the context: no arena, no pending solves, and a stream of
 // their own when a pool is open (the gather's)
-hipStream_t io_stream(of_ctx *c) {
-  if (!c->pool) return c->stream;
-  if (!c->gstream) create_stream(&c->gstream);
-  return c->gstream;
+// (the gather stream exists whenever a pool is open: of_pairs_open creates it
+// with the lanes, ensure_lanes)
+hipStream_t io_stream(of_ctx *c) { return c->pool ? c->gstream : c->stream; }
+namespace {
+void ensure_lanes(of_ctx *c, int n);
 }
+// a slot queued to the pair pool and not yet finished (pool_slot_busy)
+bool pool_slot_busy(of_ctx *c, int slot);
 #define API_BEGIN_IO(ctx)               \
   if (!ctx) return OF_EINVAL;           \
   try {                                 \
@@ -2170,8 +2173,19 @@ int of_synchronize(of_ctx *c) {
   return hipStreamSynchronize(c->stream) == hipSuccess ? OF_OK : OF_EHIP;
 }
 
+// Settings and profiling tables the pool's lanes read (lane 0 is the context
+// itself) are refused while a pair stream is open: changing them under a
+// running lane would give its pairs other arithmetic than the lanes that
+// copied them at of_pairs_open, or race the lane's own writes.
+#define REFUSE_WHILE_POOL(c)                                                          \
+  if ((c)->pool) {                                                                   \
+    (c)->err = "a pair stream is open on this context (of_pairs_close first)";       \
+    return OF_EINVAL;                                                                \
+  }
+
 int of_set_option(of_ctx *c, int option, int value) {
   if (!c) return OF_EINVAL;
+  REFUSE_WHILE_POOL(c)
   switch (option) {
     case OF_OPT_SOR_PIPELINE:
       c->opt_sor_pipe = value ? 1 : 0;
@@ -2221,6 +2235,13 @@ int of_get_option(of_ctx *c, int option, int64_t *value) {
       *value = n;
       return OF_OK;
     }
+    case OF_OPT_RCCL_NRANKS: {
+      // ranks of the context's RCCL communicator as RCCL reports them (0: none)
+      int n = 0;
+      if (c->comm && ncclCommCount(c->comm, &n) != ncclSuccess) n = -1;
+      *value = n;
+      return OF_OK;
+    }
     default:
       c->err = "unknown option";
       return OF_EINVAL;
@@ -2229,6 +2250,7 @@ int of_get_option(of_ctx *c, int option, int64_t *value) {
 
 int of_set_profiling(of_ctx *c, int enable) {
   if (!c) return OF_EINVAL;
+  REFUSE_WHILE_POOL(c)
   try {
     flush_prof(c);
   } catch (const OfError &e) {
@@ -2251,6 +2273,7 @@ int of_set_profiling(of_ctx *c, int enable) {
 
 int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t *count, double *pixels, int *n) {
   if (!c || !n) return OF_EINVAL;
+  REFUSE_WHILE_POOL(c)
   int k = 0;
   for (auto &kv : c->ktimes) {
     if (k < max) {
@@ -2268,6 +2291,7 @@ int of_kernel_times(of_ctx *c, int max, const char **names, double *ms, int64_t 
 int of_kernel_timeline(of_ctx *c, int max, const char **names, double *pixels, double *t0_ms, double *t1_ms,
                        int *n) {
   if (!c || !n) return OF_EINVAL;
+  REFUSE_WHILE_POOL(c)
   const int m = (int)c->tl.size();
   for (int k = 0; k < m && k < max; ++k) {
     if (names) names[k] = c->tl[k].name;
@@ -2281,6 +2305,7 @@ int of_kernel_timeline(of_ctx *c, int max, const char **names, double *pixels, d
 
 int of_set_solve_log(of_ctx *c, int enable) {
   if (!c) return OF_EINVAL;
+  REFUSE_WHILE_POOL(c)
   c->slog = enable ? 1 : 0;
   c->slog_rec.clear();
   return OF_OK;
@@ -2424,6 +2449,7 @@ int of_alt_ba_flow_base(of_ctx *c, of_params *P, const float *images, int H, int
 int of_pair_upload(of_ctx *c, int slot, const float *im1, const float *im2, int H, int W, int C) {
   API_BEGIN_IO(c)
   REQUIRE(slot >= 0 && slot < 4096 && im1 && im2 && (C == 1 || C == 3), OF_EINVAL, "bad arguments");
+  REQUIRE(!pool_slot_busy(c, slot), OF_EINVAL, "slot is queued in the pair stream (of_pairs_wait its ticket first)");
   if ((int)c->slots.size() <= slot) c->slots.resize(slot + 1);
   Slot &s = c->slots[slot];
   const size_t n = (size_t)H * W * C * sizeof(float), nu = 2 * (size_t)H * W;
@@ -2482,6 +2508,11 @@ void ensure_lanes(of_ctx *c, int n) {
     REQUIRE(rc == OF_OK, rc, "lane context: " + g_err);
     c->lanes.push_back(l);
   }
+  // the gather / slot-copy stream (of_rccl_gather_slots, io_stream) right
+  // after the lanes, for every run that has lanes: N = 1 and N > 1 map their
+  // streams to hardware queues the same way (one created lazily at the first
+  // gather, after the copy stream, would land on a busy lane's queue)
+  if (!c->gstream) create_stream(&c->gstream);
 }
 // profiling: the child lanes' timings into the ctx's table (lane 0, the ctx,
 // records its own)
@@ -2786,6 +2817,7 @@ struct PairJob {
   int64_t ticket;
   Slot dev;                  // ... or a device-resident slot (of_pairs_submit_slots)
   bool on_dev = false;
+  int slot = -1;             // that slot's index
 };
 }  // namespace
 
@@ -2802,8 +2834,17 @@ struct PairPool {
   bool closing = false;
   int64_t next_ticket = 0;
   std::vector<uint8_t> done;  // by ticket
+  std::map<int, int> busy;    // device slot -> its queued or running jobs (of_pairs_submit_slots)
   OfError err{OF_OK, ""};
 };
+
+extern "C++" bool pool_slot_busy(of_ctx *c, int slot) {
+  PairPool *pp = c->pool;
+  if (!pp) return false;
+  std::lock_guard<std::mutex> lk(pp->m);
+  auto it = pp->busy.find(slot);
+  return it != pp->busy.end() && it->second > 0;
+}
 
 void pool_set_progress(PairPool *pp, of_progress_fn fn) { pp->prog_fn = fn; }
 
@@ -2847,6 +2888,7 @@ void pool_lane(of_ctx *c, PairPool *pp, int li) {
     }
     {
       std::lock_guard<std::mutex> lk(pp->m);
+      if (j.on_dev) --pp->busy[j.slot];
       pp->done[j.ticket] = 1;
     }
     pp->cv_done.notify_all();
@@ -3052,6 +3094,15 @@ int of_pairs_submit_slots(of_ctx *c, int n, const int *slots, int64_t *first_tic
       c->err = "pair stream closing";
       return OF_EINVAL;
     }
+    for (int k = 0; k < n; ++k) {
+      auto it = pp->busy.find(slots[k]);
+      int dup = 0;
+      for (int q = 0; q < k; ++q) dup += slots[q] == slots[k];
+      if ((it != pp->busy.end() && it->second > 0) || dup) {
+        c->err = "slot already queued in the pair stream (of_pairs_wait its ticket first)";
+        return OF_EINVAL;
+      }
+    }
     if (first_ticket) *first_ticket = pp->next_ticket;
     for (int k = 0; k < n; ++k) {
       PairJob j;
@@ -3060,6 +3111,8 @@ int of_pairs_submit_slots(of_ctx *c, int n, const int *slots, int64_t *first_tic
       j.ticket = pp->next_ticket++;
       j.dev = c->slots[slots[k]];
       j.on_dev = true;
+      j.slot = slots[k];
+      ++pp->busy[slots[k]];
       pp->q.push_back(j);
       pp->done.push_back(0);
     }
@@ -3121,6 +3174,7 @@ int of_pairs_close(of_ctx *c) {
 int of_pair_download(of_ctx *c, int slot, float *out_uv) {
   API_BEGIN_IO(c)
   REQUIRE(slot >= 0 && slot < (int)c->slots.size() && c->slots[slot].uv && out_uv, OF_EINVAL, "bad slot");
+  REQUIRE(!pool_slot_busy(c, slot), OF_EINVAL, "slot is queued in the pair stream (of_pairs_wait its ticket first)");
   Slot &s = c->slots[slot];
   HIPCHK(hipMemcpyAsync(out_uv, s.uv, sizeof(float) * 2 * (size_t)s.H * s.W, hipMemcpyDeviceToHost, ios));
   HIPCHK(hipStreamSynchronize(ios));
@@ -3142,6 +3196,7 @@ int of_rccl_init(of_ctx *c, const char *id128, int nranks, int rank) {
   REQUIRE(id128 && nranks >= 1 && rank >= 0 && rank < nranks, OF_EINVAL, "bad arguments");
   ncclUniqueId id;
   memcpy(&id, id128, 128);
+  ensure_lanes(c, 0);  // the lanes and the gather stream, in the order a pool would create them
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
   REQUIRE(r == ncclSuccess, OF_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   c->nranks = nranks;
@@ -3164,7 +3219,7 @@ int of_rccl_gather_slots(of_ctx *c, int first, int nslots, float *out_uv_rank0) 
   try {
   HIPCHK(hipSetDevice(c->device));
   REQUIRE(c->comm, OF_EINVAL, "of_rccl_init first");
-  if (!c->gstream) create_stream(&c->gstream);
+  if (!c->gstream) ensure_lanes(c, 0);  // (never while a pool is open: of_pairs_open made it)
   REQUIRE(first >= 0 && nslots >= 1 && first + nslots <= (int)c->slots.size(), OF_EINVAL, "bad slot range");
   Slot *sl = c->slots.data() + first;
   const int H = sl[0].H, W = sl[0].W;
@@ -3413,6 +3468,59 @@ int of_weighted_median(of_ctx *c, const float *uv, const float *guide, int gc, c
   wmf(c, f, g, oc.p, o, area_hsz, sigma_i);
   download_f2(c, o, out);
   HIPCHK(hipStreamSynchronize(c->stream));
+  API_END(c)
+}
+
+// flow_to_color (viz/flow_color.py:77-107): the wheel of make_colorwheel
+// (flow_color.py:5-40) built on the host, the radius reduction and the
+// per-pixel map on the device (k_flow_rad_max, k_flow_color)
+}  // extern "C"
+namespace {
+ColorWheel color_wheel() {
+  ColorWheel cw{};
+  const int n[6] = {15, 6, 4, 11, 13, 6};
+  // per segment: the channel held at 255, the ramped channel and whether it ramps down
+  const int hold[6] = {0, 1, 1, 2, 2, 0}, ramp[6] = {1, 0, 2, 1, 0, 2};
+  int k = 0;
+  for (int s = 0; s < 6; ++s)
+    for (int i = 0; i < n[s]; ++i, ++k) {
+      const double r = std::floor(255.0 * i / n[s]);  // np.floor(255 * np.arange(n) / n)
+      cw.w[3 * k + hold[s]] = 255;
+      cw.w[3 * k + ramp[s]] = (unsigned char)(s % 2 ? 255.0 - r : r);
+    }
+  return cw;
+}
+template <typename T>
+void flow_color_dev(of_ctx *c, const void *flow, long n, double fixed, uint8_t *out) {
+  using U = typename OrdBits<T>::U;
+  T *d = (T *)c->arena.alloc(sizeof(T) * 2 * n);
+  U *mx = (U *)c->arena.alloc(sizeof(U));
+  unsigned char *o = (unsigned char *)c->arena.alloc(3 * n);
+  HIPCHK(hipMemcpyAsync(d, flow, sizeof(T) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(mx, 0, sizeof(U), c->stream));
+  const int blocks = (int)std::min<long>((n + 255) / 256, 2048);
+  c->cur_px = (double)n;
+  if (fixed <= 0) launch(c, "flow_rad_max", k_flow_rad_max<T>, dim3(blocks), dim3(256), 0, (const T *)d, n, mx);
+  launch(c, "flow_color", k_flow_color<T>, dim3(blocks), dim3(256), 0, (const T *)d, n, (const U *)mx, fixed,
+         color_wheel(), o);
+  HIPCHK(hipMemcpyAsync(out, o, 3 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+}
+}  // namespace
+extern "C" {
+
+int of_flow_to_color(of_ctx *c, const void *flow, int dtype, int H, int W, int has_max, double max_flow,
+                     uint8_t *out_rgb) {
+  API_BEGIN(c)
+  REQUIRE(H >= 0 && W >= 0 && (dtype == 0 || dtype == 1) && (H * (long)W == 0 || (flow && out_rgb)), OF_EINVAL,
+          "bad arguments");
+  const long n = (long)H * W;
+  // max_rad = max(max_flow, 1e-8) (flow_color.py:100): > 0 selects the fixed value
+  const double fixed = has_max ? (max_flow > 1e-8 ? max_flow : 1e-8) : 0.0;
+  if (n > 0) {
+    if (dtype == 0) flow_color_dev<float>(c, flow, n, fixed, out_rgb);
+    else flow_color_dev<double>(c, flow, n, fixed, out_rgb);
+  }
   API_END(c)
 }
 

@@ -369,3 +369,99 @@ __global__ void k_sub_scaled(const float *__restrict__ a, const float *__restric
     out[k] = a[k] - alp * b[k];
   }
 }
+
+// ---------------------------------------------------------------------------
+// Middlebury flow colour coding (viz/flow_color.py:43-107; SURVEY.md §8f row
+// 4).  One pass reduces the largest known radius, one maps each pixel through
+// the 55-bin wheel.  The arithmetic follows numpy's dtype rules step by step,
+// so the uint8 image equals the reference's: T = the flow's dtype for
+// the normalisation, the radius, atan2(-v, -u) / pi and fk = (a + 1) / 2 * 54;
+// f = fk - k0 and the colour blend in float64 (float32 - int64 promotes).  No
+// contraction into fma: numpy rounds every product and sum on its own.
+struct ColorWheel {
+  unsigned char w[55 * 3];  // make_colorwheel (flow_color.py:5-40), RGB per bin
+};
+
+template <typename T> struct OrdBits;
+template <> struct OrdBits<float> {
+  using U = unsigned int;
+  static __device__ U of(float x) { return __float_as_uint(x); }
+  static __device__ float to(U b) { return __uint_as_float(b); }
+};
+template <> struct OrdBits<double> {
+  using U = unsigned long long;
+  static __device__ U of(double x) { return (U)__double_as_longlong(x); }
+  static __device__ double to(U b) { return __longlong_as_double((long long)b); }
+};
+
+// largest sqrt(u^2 + v^2) over pixels with |u|, |v| <= 1e9 (flow_color.py:92-98);
+// radii are >= 0, so their bit patterns order like the values (*mx starts at 0)
+template <typename T>
+__global__ void k_flow_rad_max(const T *__restrict__ flow, long n, typename OrdBits<T>::U *mx) {
+#pragma clang fp contract(off)
+  using U = typename OrdBits<T>::U;
+  U best = 0;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < n; p += (long)gridDim.x * blockDim.x) {
+    const T u = flow[2 * p], v = flow[2 * p + 1];
+    if (fabs(u) > (T)1e9 || fabs(v) > (T)1e9) continue;
+    const T r = sqrt(u * u + v * v);
+    const U b = OrdBits<T>::of(r);
+    best = b > best ? b : best;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const U o = __shfl_down(best, off, 64);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(mx, best);
+}
+
+// max_rad = max(max_rad, 1e-8) (flow_color.py:100) in T: the fixed max_flow
+// (fixed > 0) or the reduced radius
+template <typename T>
+__device__ __forceinline__ T color_max_rad(const typename OrdBits<T>::U *mx, double fixed) {
+  if (fixed > 0) return (T)(fixed > 1e-8 ? fixed : 1e-8);
+  const T r = OrdBits<T>::to(*mx);
+  return (T)1e-8 > r ? (T)1e-8 : r;
+}
+
+template <typename T>
+__device__ __forceinline__ T color_atan2(T y, T x);
+// float32: numpy's float32 arctan2 on the host is a vector-library routine
+// (not correctly rounded, and CPU-dependent); the device rounds the float64
+// atan2 to float32, the correctly rounded value (tests/test_gpu_viz.py states
+// what that leaves)
+template <> __device__ __forceinline__ float color_atan2<float>(float y, float x) {
+  return (float)atan2((double)y, (double)x);
+}
+template <> __device__ __forceinline__ double color_atan2<double>(double y, double x) { return atan2(y, x); }
+
+template <typename T>
+__global__ void k_flow_color(const T *__restrict__ flow, long n, const typename OrdBits<T>::U *mx, double fixed,
+                             ColorWheel cw, unsigned char *__restrict__ out) {
+#pragma clang fp contract(off)
+  const T mr = color_max_rad<T>(mx, fixed);
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < n; p += (long)gridDim.x * blockDim.x) {
+    T u = flow[2 * p], v = flow[2 * p + 1];
+    unsigned char rgb[3] = {0, 0, 0};
+    if (!(fabs(u) > (T)1e9 || fabs(v) > (T)1e9)) {  // unknown flow stays black (:105)
+      u = u / mr;
+      v = v / mr;
+      const T rad = sqrt(u * u + v * v);
+      const T a = color_atan2<T>(-v, -u) / (T)3.141592653589793;
+      const T fk = (a + (T)1) / (T)2 * (T)54;
+      const int k0 = (int)floor(fk);
+      const int k1 = k0 + 1 == 55 ? 0 : k0 + 1;
+      const double f = (double)fk - (double)k0;
+      for (int c = 0; c < 3; ++c) {
+        double col = (double)cw.w[3 * k0 + c] / 255.0 * (1.0 - f) + (double)cw.w[3 * k1 + c] / 255.0 * f;
+        col = 1.0 - (double)rad * (1.0 - col);
+        if (rad > (T)1) col = col * 0.75;
+        col = col < 0.0 ? 0.0 : (col > 1.0 ? 1.0 : col);
+        rgb[c] = (unsigned char)floor(255.0 * col);
+      }
+    }
+    out[3 * p] = rgb[0];
+    out[3 * p + 1] = rgb[1];
+    out[3 * p + 2] = rgb[2];
+  }
+}

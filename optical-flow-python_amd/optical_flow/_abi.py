@@ -23,6 +23,7 @@ OF_OPT_SOR_PIPELINE = 1  # of_set_option
 OF_OPT_SOR_FALLBACKS = 2  # of_get_option (read-only counter)
 OF_OPT_FUSED_WARP = 3  # of_set_option: warp + assembly in one kernel (default 1)
 OF_OPT_DEVICE_BYTES = 4  # of_get_option (read-only): grow-only device bytes of the context and its lanes
+OF_OPT_RCCL_NRANKS = 5  # of_get_option (read-only): ranks of the RCCL communicator (ncclCommCount; 0 = none)
 
 
 class OfPenalty(C.Structure):

@@ -78,6 +78,7 @@ _SIGS = {
     "of_detect_occlusion": ([_vp, _fp, _fp, C.c_int, C.c_int, C.c_int, _fp], C.c_int),
     "of_weighted_median": ([_vp, _fp, _fp, C.c_int, _fp, C.c_int, C.c_int, C.c_int, C.c_double, _fp], C.c_int),
     "of_median_filter": ([_vp, _fp, C.c_int, C.c_int, C.c_int, C.c_int, _fp], C.c_int),
+    "of_flow_to_color": ([_vp, _vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, _vp], C.c_int),
     "of_solver_geometry": ([C.c_int, C.c_int, C.c_int, C.POINTER(OfCgGeometry)], C.c_int),
     "of_set_solve_log": ([_vp, C.c_int], C.c_int),
     "of_solve_log": ([_vp, C.c_int, C.POINTER(OfSolveRecord), _ip], C.c_int),

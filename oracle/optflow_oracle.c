@@ -580,13 +580,18 @@ static double dotp(const double *a, const double *b, long n) {
 /* scipy.sparse.linalg.cg with a Jacobi (block=0) or 2x2-block-Jacobi (block=1)
  * preconditioner, x0 = 0 (base.py:116-136) */
 static int pcg(const double *coef, const double *b, int H, int W, double rtol, int maxiter, int block,
-               double *x, double *relres) {
+               const double *x0, double *x, double *relres) {
   long N = (long)H * W, n2 = 2 * N;
   double *r = malloc(n2 * sizeof(double)), *z = malloc(n2 * sizeof(double));
   double *p = malloc(n2 * sizeof(double)), *q = malloc(n2 * sizeof(double));
   double bn = sqrt(dotp(b, b, n2)), atol = rtol * bn;
   memset(x, 0, n2 * sizeof(double));
   memcpy(r, b, n2 * sizeof(double));
+  if (x0) { /* warm start (experiment knob ofr_set_warm_start): r = b - A x0 */
+    memcpy(x, x0, n2 * sizeof(double));
+    op_apply(coef, H, W, x0, q);
+    for (long k = 0; k < n2; ++k) r[k] = b[k] - q[k];
+  }
   int it = 0;
   double rho_prev = 0;
   if (bn == 0) { *relres = 0; free(r); free(z); free(p); free(q); return 0; }
@@ -661,15 +666,38 @@ void ofr_set_backslash_rtol(double rtol) { g_backslash_rtol = rtol > 0 ? rtol : 
  * what fp32 storage of x alone does to the chaotic family. */
 static int g_round_x_f32 = 0;
 void ofr_set_round_x_f32(int on) { g_round_x_f32 = on != 0; }
+/* ofr_set_warm_start (test-only experiment knob, tools/warm_start_iters.py):
+ * the starting iterate of the 'backslash' PCG in irls_base's warps after the
+ * first of a level (the reference's spsolve takes none, base.py:107-108, so
+ * its answer does not depend on it; only the iteration count does).
+ *   0  x0 = 0 (the default)
+ *   1  the previous warp's unclipped solution
+ *   2  (uv_prev + x_prev, before the filter) - uv: the part of the previous
+ *      step the median filter took back
+ *   +10  the same direction scaled by gamma = x0.b / x0.A x0 (the A-norm
+ *        optimal multiple; gamma x0 is never worse than 0 in the A-norm)
+ * ofr_solve_log: per solve (H, W, warp index, iterations, 1000 * alpha) */
+static int g_warm = 0;
+static const double *g_x0 = NULL;
+void ofr_set_warm_start(int mode) { g_warm = mode; }
+#define OFR_SLOG_MAX 4096
+static int g_slog[OFR_SLOG_MAX][5];
+static int g_slog_n = 0;
+int ofr_solve_log(int *out, int max) {
+  int n = g_slog_n < max ? g_slog_n : max;
+  if (out) memcpy(out, g_slog, (size_t)n * 5 * sizeof(int));
+  g_slog_n = 0;
+  return n;
+}
 
 int ofr_solve(const of_params *P, const double *coef, const double *rhs, int H, int W, double *x, int *iters,
               double *relres) {
   double rr = 0;
   int it;
-  if (P->solver == OF_SOLVER_PCG) it = pcg(coef, rhs, H, W, P->pcg_rtol, P->pcg_maxiter, 0, x, &rr);
+  if (P->solver == OF_SOLVER_PCG) it = pcg(coef, rhs, H, W, P->pcg_rtol, P->pcg_maxiter, 0, NULL, x, &rr);
   else if (P->solver == OF_SOLVER_SOR) it = sor(coef, rhs, H, W, 1.9, P->sor_max_iters, 1e-2, x);
   else {
-    it = pcg(coef, rhs, H, W, g_backslash_rtol, 100000, 1, x, &rr);
+    it = pcg(coef, rhs, H, W, g_backslash_rtol, 100000, 1, g_x0, x, &rr);
     if (g_round_x_f32)
       for (long k = 0; k < 2L * H * W; ++k) x[k] = (double)(float)x[k];
   }
@@ -875,6 +903,8 @@ static void irls_base(drv_t *d, const level_t *L, double *uv, double alpha, int 
   double *coef = malloc(7 * N * sizeof(double)), *rhs = malloc(2 * N * sizeof(double)), *x = malloc(2 * N * sizeof(double));
   double *duv = malloc(2 * N * sizeof(double)), *uv1 = malloc(2 * N * sizeof(double)), *occ = malloc(N * sizeof(double));
   double *tmp = malloc(2 * N * sizeof(double));
+  double *xw = malloc(2 * N * sizeof(double)), *xp = malloc(2 * N * sizeof(double));
+  double *upre = malloc(2 * N * sizeof(double));
   double blend = P->method == OF_METHOD_BA ? P->blend : 0.5; /* classic_nl.py:232 passes no blend */
   for (int i = 0; i < P->max_iters; ++i) {
     memset(duv, 0, 2 * N * sizeof(double));
@@ -882,8 +912,25 @@ static void irls_base(drv_t *d, const level_t *L, double *uv, double alpha, int 
     for (int j = 0; j < max_linear; ++j) {
       ofr_flow_operator(P, alpha, uv, duv, It, Ix, Iy, H, W, nc, coef, rhs);
       int it;
+      g_x0 = NULL;
+      if (g_warm % 10 && i > 0 && j == 0) {
+        for (long k = 0; k < 2 * N; ++k) xw[k] = g_warm % 10 == 1 ? xp[k] : upre[k] - uv[k];
+        if (g_warm >= 10) {
+          op_apply(coef, H, W, xw, tmp);
+          double xAx = dotp(xw, tmp, 2 * N), xb = dotp(xw, rhs, 2 * N), gam = xAx > 0 ? xb / xAx : 0.0;
+          for (long k = 0; k < 2 * N; ++k) xw[k] *= gam;
+        }
+        g_x0 = xw;
+      }
       ofr_solve(P, coef, rhs, H, W, x, &it, NULL);
+      g_x0 = NULL;
       note_solve(d, it);
+      if (g_slog_n < OFR_SLOG_MAX) {
+        int *e = g_slog[g_slog_n++];
+        e[0] = H; e[1] = W; e[2] = i; e[3] = it; e[4] = (int)lround(alpha * 1000);
+      }
+      memcpy(xp, x, 2 * N * sizeof(double));
+      for (long k = 0; k < 2 * N; ++k) upre[k] = uv[k] + x[k];
       if (P->limit_update) clip_update(x, 2 * N);
       for (long k = 0; k < 2 * N; ++k) uv1[k] = uv[k] + x[k];
       if (P->median_filter_size) {
@@ -900,6 +947,7 @@ static void irls_base(drv_t *d, const level_t *L, double *uv, double alpha, int 
     for (long k = 0; k < 2 * N; ++k) uv[k] += duv[k];
   }
   free(It); free(Ix); free(Iy); free(coef); free(rhs); free(x); free(duv); free(uv1); free(occ); free(tmp);
+  free(xw); free(xp); free(upre);
 }
 
 /* denoise_LO (denoising.py:6-30) */

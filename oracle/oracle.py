@@ -45,6 +45,8 @@ def lib():
         _lib.ofr_num_threads.restype = C.c_int
         _lib.ofr_set_backslash_rtol.argtypes = [C.c_double]
         _lib.ofr_set_round_x_f32.argtypes = [C.c_int]
+        _lib.ofr_set_warm_start.argtypes = [C.c_int]
+        _lib.ofr_solve_log.argtypes = [C.POINTER(C.c_int), C.c_int]
     return _lib
 
 
@@ -77,6 +79,20 @@ def set_round_x_f32(on):
     """Test-only experiment knob (tools/rtol_chaos.py): round every
     'backslash' solution to float32, as the GPU returns it."""
     lib().ofr_set_round_x_f32(C.c_int(1 if on else 0))
+
+
+def set_warm_start(mode):
+    """Test-only experiment knob (tools/warm_start_iters.py): the starting
+    iterate of the 'backslash' PCG in warps after a level's first (0 = zero,
+    the default; see ofr_set_warm_start in optflow_oracle.c)."""
+    lib().ofr_set_warm_start(C.c_int(int(mode)))
+
+
+def solve_log():
+    """Per-solve records since the last call: (H, W, warp, iterations, alpha)."""
+    buf = (C.c_int * (5 * 4096))()
+    n = lib().ofr_solve_log(buf, 4096)
+    return [(buf[5 * k], buf[5 * k + 1], buf[5 * k + 2], buf[5 * k + 3], buf[5 * k + 4] / 1000.0) for k in range(n)]
 
 
 def num_threads():

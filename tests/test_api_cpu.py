@@ -171,7 +171,7 @@ def test_metrics_known_answers():
 
 
 def test_flow_to_color():
-    from optical_flow import flow_to_color
+    from oracle_viz import flow_to_color  # the HIP path's checker (tests/test_gpu_viz.py)
     f = np.random.default_rng(2).normal(size=(20, 30, 2)) * 3
     f[0, 0, 0] = 2e9
     img = flow_to_color(f)
@@ -179,13 +179,14 @@ def test_flow_to_color():
 
 
 def test_flow_to_color_vs_reference(golden):
-    """flow_to_color (viz/flow_color.py:43-107) bit-exact against the
-    reference's images (tests/golden/gen_golden.py viz_metrics): RubberWhale
-    GT with 7244 unknown entries (auto and fixed max_flow), the reference's
-    own RubberWhale uv in float32 (coloured in float32) and float64, a
-    synthetic field with unknown rows/entries and rad > 1 saturation, and an
-    all-zero field."""
-    from optical_flow import flow_to_color, read_flo
+    """The oracle's flow_to_color (oracle/oracle_viz.py, the checker of the
+    HIP path; viz/flow_color.py:43-107) bit-exact against the reference's
+    images (tests/golden/gen_golden.py viz_metrics): RubberWhale GT with 7244
+    unknown entries (auto and fixed max_flow), the reference's own RubberWhale
+    uv in float32 (coloured in float32) and float64, a synthetic field with
+    unknown rows/entries and rad > 1 saturation, and an all-zero field."""
+    from oracle_viz import flow_to_color
+    from optical_flow import read_flo
     d = golden("viz_metrics.npz")
     gt = read_flo(os.path.join(ROOT, "tests", "golden", "flow10.flo"))
     rw = golden("rubberwhale_ref.npz")

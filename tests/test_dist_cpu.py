@@ -162,3 +162,48 @@ def test_inner_loop_figure():
     assert r["kernel_ms_per_step"] == 13.0  # wmf excluded, pcg_small counted
     assert r["frac"] == pytest.approx(byt / 13e-3 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
     assert r["finest"]["frac"] == pytest.approx(byt / 12.5e-3 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def _run_bench(args, env, timeout=240):
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, [json.loads(ln) for ln in lines]
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts
+    torch.distributed.run with two processes (a child, no exec), each rank
+    rendezvouses over gloo, and rank 0's line -- relayed once by the parent --
+    reports n_gpus 2 and both ranks (--dry-run stops before the library)."""
+    r, recs = _run_bench(["--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "0"], _bench_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    assert sorted(map(tuple, rec["ranks"])) == [(0, 0, 2), (1, 1, 2)]
+    assert rec["max_over_ranks"] == pytest.approx(0.002)
+    assert "torch.distributed.run child, 2 processes" in rec["launch"]
+
+
+def test_bench_gpus1_runs_in_process():
+    r, recs = _run_bench(["--gpus", "1", "--dry-run"], _bench_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(recs) == 1 and recs[0]["n_gpus"] == 1 and recs[0]["ranks"] == [[0, 0, 1]]
+    assert "launch" not in recs[0]
+
+
+def test_bench_world_size_mismatch_refused():
+    r, recs = _run_bench(["--gpus", "1", "--dry-run"], _bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and not recs
+    assert "WORLD_SIZE=2 but --gpus 1" in r.stderr
+    r, recs = _run_bench(["--gpus", "2", "--rccl-self", "--dry-run"], _bench_env(WORLD_SIZE="2"))
+    assert r.returncode == 2 and not recs

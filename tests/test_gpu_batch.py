@@ -209,6 +209,10 @@ def test_rccl_gather_while_pool_computes():
     uid = C.create_string_buffer(128)
     ctx.check(lib.of_rccl_unique_id(uid))
     ctx.check(lib.of_rccl_init(ctx.handle, uid.raw, 1, 0))
+    from optical_flow import _abi
+    nr = C.c_int64(0)
+    ctx.check(lib.of_get_option(ctx.handle, _abi.OF_OPT_RCCL_NRANKS, C.byref(nr)))
+    assert nr.value == 1  # RCCL's own count (ncclCommCount)
     sets = [(C.c_int * n)(*range(k * n, (k + 1) * n)) for k in range(2)]
     gathered = []
     try:
@@ -300,3 +304,57 @@ def test_pairs_run_host_fine_solves_side_by_side():
     print(f"lanes vs single 1080p: mean {e.mean():.2e} p99 {np.percentile(e, 99):.2e} "
           f"dAEPE {abs(aepe(got2[0]) - aepe(ref)):.2e}")
     assert e.mean() < 1e-3 and abs(aepe(got2[0]) - aepe(ref)) < 1e-4
+
+
+def test_pool_refuses_settings_and_busy_slots():
+    """While a pair stream is open (lane 0 = the context), the settings and
+    profiling calls the lanes read are refused, and a slot queued in the
+    stream cannot be submitted again, re-uploaded or downloaded until its
+    ticket is done (a re-upload could free the frames under a
+    running lane).  One lane, two 540x960 pairs: the second pair waits
+    behind the first for tens of ms, inside which every check runs."""
+    from optical_flow import _abi, _native
+    from optical_flow.utils.synthetic import synth_pair
+    ctx = _native.Context(0)
+    lib = ctx.lib
+    H, W = 540, 960
+    a, b = synth_pair(H, W, 5)[:2]
+    fa, fb = _native.f32(a), _native.f32(b)
+    for s in range(2):
+        ctx.check(lib.of_pair_upload(ctx.handle, s, _native.ptr(fa), _native.ptr(fb), H, W, 3))
+    P0 = _params("classic+nl-fast")
+    slots = (C.c_int * 2)(0, 1)
+    dup = (C.c_int * 2)(0, 0)
+    ctx.check(lib.of_pairs_open(ctx.handle, H, W, 3, C.byref(P0), 1))
+    try:
+        with pytest.raises(ValueError):
+            ctx.check(lib.of_pairs_submit_slots(ctx.handle, 2, dup, None))
+        t = C.c_int64(0)
+        ctx.check(lib.of_pairs_submit_slots(ctx.handle, 2, slots, C.byref(t)))
+        uv = np.empty((2, H, W), np.float32)
+        with pytest.raises(ValueError, match="queued"):
+            ctx.check(lib.of_pairs_submit_slots(ctx.handle, 1, (C.c_int * 1)(1), None))
+        with pytest.raises(ValueError, match="queued"):
+            ctx.check(lib.of_pair_upload(ctx.handle, 1, _native.ptr(fa), _native.ptr(fb), H, W, 3))
+        with pytest.raises(ValueError, match="queued"):
+            ctx.check(lib.of_pair_download(ctx.handle, 1, _native.ptr(uv)))
+        n = C.c_int(0)
+        for call in (lambda: lib.of_set_option(ctx.handle, _abi.OF_OPT_FUSED_WARP, 0),
+                     lambda: lib.of_set_profiling(ctx.handle, 1),
+                     lambda: lib.of_set_solve_log(ctx.handle, 1),
+                     lambda: lib.of_kernel_times(ctx.handle, 0, None, None, None, None, C.byref(n)),
+                     lambda: lib.of_kernel_timeline(ctx.handle, 0, None, None, None, None, C.byref(n))):
+            with pytest.raises(ValueError, match="pair stream is open"):
+                ctx.check(call())
+        for tk in (t.value, t.value + 1):
+            ctx.check(lib.of_pairs_wait(ctx.handle, tk))
+        # done: the slot is free again
+        ctx.check(lib.of_pair_download(ctx.handle, 1, _native.ptr(uv)))
+        ctx.check(lib.of_pairs_submit_slots(ctx.handle, 1, (C.c_int * 1)(1), C.byref(t)))
+        ctx.check(lib.of_pairs_wait(ctx.handle, t.value))
+    finally:
+        ctx.check(lib.of_pairs_close(ctx.handle))
+    ctx.check(lib.of_set_option(ctx.handle, _abi.OF_OPT_FUSED_WARP, 1))
+    v = C.c_int64(-1)
+    ctx.check(lib.of_get_option(ctx.handle, _abi.OF_OPT_RCCL_NRANKS, C.byref(v)))
+    assert v.value == 0  # no communicator on this context
