@@ -514,6 +514,39 @@ def as_timed_of(timeline, per_level, dom, fine):
                       "union of the launches' intervals (tools/side_by_side_rocprof.py's method)"}
 
 
+# kernels that run before the level loop (preprocessing, ROF, pyramids):
+# keyed by a level's pixel count too, but outside its compute_flow_base time
+PRE_LEVEL = ("rof_iters", "correlate", "resize", "minmax", "mm_init", "scale", "rgb_max", "rgb_prep", "sub_scaled")
+
+
+def level_breakdown(levels, per_level, pairs):
+    """Per pyramid level of one serial pair: the wall time of resample +
+    compute_flow_base (HIP events around the level, of_stats.level_ms) beside
+    the HIP-event kernel time of the same level in the lanes = 1 replay
+    (per pair); `gap_ms` = wall - kernels = launch gaps + host syncs (e.g. HS's
+    ||x|| < 1e-3 exit read, hs.py:127-128).  For SOR: sweeps and us per sweep
+    of the pipelined solve (sor_pipe.active = sweeps x level pixels)."""
+    out = []
+    for px in sorted({l["h"] * l["w"] for l in levels}):
+        wall = sum(l["ms"] for l in levels if l["h"] * l["w"] == px)
+        ks = {n: r["ms_total"] / pairs for (n, p), r in per_level.items()
+              if p == px and not n.endswith(".active") and n not in PRE_LEVEL}
+        kern = sum(ks.values())
+        lv = next(l for l in levels if l["h"] * l["w"] == px)
+        rec = {"h": lv["h"], "w": lv["w"], "wall_ms": round(wall, 3), "kernel_ms": round(kern, 3),
+               "gap_ms": round(wall - kern, 3), "gap_share": round((wall - kern) / wall, 4) if wall > 0 else None,
+               "top": {n: round(v, 3) for n, v in sorted(ks.items(), key=lambda kv: -kv[1])[:4]}}
+        for solver in ("sor_pipe", "sor_sweep"):
+            if (solver, px) in per_level:
+                sw = per_level.get((solver + ".active", px), per_level[(solver, px)])["px"] / px / pairs
+                ms = per_level[(solver, px)]["ms_total"] / pairs
+                rec.update({"solver": solver, "solver_ms": round(ms, 3), "sweeps": round(sw, 2),
+                            "solves": per_level[(solver, px)]["launches"] / pairs,
+                            "us_per_sweep": round(1e3 * ms / sw, 2) if sw else None})
+        out.append(rec)
+    return out
+
+
 def kms(kt, pairs, top=14):
     return {k: round(v["ms_total"] / pairs, 3) for k, v in
             sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])[:top] if not k.endswith(".active")}
@@ -739,6 +772,7 @@ def main(argv=None):
 
     roofline = None
     ktimes, kt_iso = {}, {}
+    pl_iso = {}
     pcg_levels = None
     inner = None
     if not args.no_profile:
@@ -753,7 +787,7 @@ def main(argv=None):
         # kernel's duration is its own, not stretched by another lane's
         # kernels sharing the CUs (profiles/: rocprofv3 of bench.py --lanes 1)
         kt1, pl1 = profiled_replay(ctx, lib, P0, args.pairs, 1)
-        kt_iso = kt1
+        kt_iso, pl_iso = kt1, pl1
         roofline = roofline_of(kt1, pl1)
         if roofline is not None:
             roofline["replay"] = "isolated: lanes=1 over the step's pairs"
@@ -822,6 +856,9 @@ def main(argv=None):
             "solver_iters_total": sd["solver_iters_total"],
             "solver_iters_max": sd["solver_iters_max"], "solves": sd["solves"],
             "pcg_per_level": pcg_levels,
+            "level_breakdown": level_breakdown(
+                [{"h": l["h"], "w": l["w"], "ms": l["ms"]} for l in sd["levels"]], pl_iso, args.pairs)
+            if pl_iso else None,
             # HIP-event kernel time per pair: isolated = the lanes=1 replay
             # (sums to <= the serial pair time); concurrent = the lanes replay
             # as timed, where durations include co-running lanes' kernels

@@ -1299,7 +1299,7 @@ void wmf(of_ctx *c, const F2 &uv, const Img &guide, const float *occ, const F2 &
   int npow2 = 64;
   while (npow2 < nreg) npow2 <<= 1;
   const int nper = npow2 / 64;  // sort keys per lane: 1..16
-  const size_t shm = 2 * WMF_NC * 64 * sizeof(wmf_sum_t) + (size_t)RW * RP * (guide.C == 3 ? 16 : 8) +
+  const size_t shm = 2 * (size_t)wmf_nc(npow2) * 64 * sizeof(wmf_sum_t) + (size_t)RW * RP * (guide.C == 3 ? 16 : 8) +
                      2 * (size_t)npow2 * sizeof(uint16_t) + 2 * (size_t)RW * RP;
   dim3 grid((uv.W + WMF_T - 1) / WMF_T, (uv.H + WMF_T - 1) / WMF_T);
   const float nk = (float)(-1.4426950408889634 / (2.0 * sigma_i * sigma_i));  // -log2(e) / (2 sigma^2)

@@ -569,6 +569,13 @@ extern __device__ unsigned long long g_wmf_t[];
 #define WMF_STAMP(i)
 #endif
 #define WMF_NC 8
+// chunks per list of the large regions (>= 512 keys, area_hsz >= 7): 16
+// halves the crossing-chunk walk (32 samples per list instead of 64) for
+// twice the chunk-sum LDS (16 KB per wave: 5 instead of 8 waves per CU)
+#ifndef WMF_NC_BIG
+#define WMF_NC_BIG 8
+#endif
+__host__ __device__ constexpr int wmf_nc(int nkeys) { return nkeys >= 512 ? WMF_NC_BIG : WMF_NC; }
 // WMF_CID_PAIR: the u- and v-list chunk ids of a region sample side by side
 // ([RW][RP][2] u8, one u16 read per window sample) instead of two planes
 // ([2][RW][RP] u8, two u8 reads)
@@ -839,7 +846,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
                                              int P, size_t ps, int hsz_rt, float nk, int RW_rt, int RP_rt,
                                              const float2 *base) {
   using T = typename WmfRec<GC>::T;
-  constexpr int N = NPER * 64, CH = N / WMF_NC;
+  constexpr int N = NPER * 64, NC = wmf_nc(N), CH = N / NC;
   const int hsz = HS > 0 ? HS : hsz_rt;
   // region width and record pitch: compile-time with HS (no runtime divides)
   constexpr int RWc = WMF_T + 2 * HS, RPc = RWc + ((8 - RWc) % 16 + 16) % 16;
@@ -857,7 +864,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // window pass reads both with one u16 load)
   extern __shared__ double lds_f64[];
   wmf_sum_t *csum = reinterpret_cast<wmf_sum_t *>(lds_f64);
-  T *smp = reinterpret_cast<T *>(csum + 2 * WMF_NC * 64);
+  T *smp = reinterpret_cast<T *>(csum + 2 * NC * 64);
   uint16_t *ku = reinterpret_cast<uint16_t *>(smp + RW * RP), *kv = ku + N;
   uint8_t *cid = reinterpret_cast<uint8_t *>(kv + N);
   int tbx = blockIdx.x, tby = blockIdx.y;
@@ -912,7 +919,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   }
   wmf_sum_t *cs = csum + lane;
 #pragma unroll
-  for (int c = 0; c < 2 * WMF_NC; ++c) cs[c * 64] = 0.0;
+  for (int c = 0; c < 2 * NC; ++c) cs[c * 64] = 0.0;
   WMF_STAMP(1);
   bitonic_regs2<NPER>(a, b, lane);
 #pragma unroll
@@ -965,7 +972,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       if (dx < n) {
         const wmf_sum_t w = (wmf_sum_t)wmf_w(rec[dx], c01, cg[2], nk);
         atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cu[dx] << WMF_SUM_SHIFT)), w);
-        atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + WMF_NC * 64, w);
+        atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + NC * 64, w);
       }
   };
   if (HS > 0) {
@@ -976,11 +983,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       for (int dx = 0; dx <= 2 * hsz; dx += 5) visit_row(qb + dy * RP + dx, min(5, 2 * hsz + 1 - dx));
   }
   WMF_STAMP(3);
-  double su[WMF_NC], sv[WMF_NC], tot = 0.0;
+  double su[NC], sv[NC], tot = 0.0;
 #pragma unroll
-  for (int c = 0; c < WMF_NC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     su[c] = cs[c * 64];
-    sv[c] = cs[(WMF_NC + c) * 64];
+    sv[c] = cs[(NC + c) * 64];
     tot += su[c];
   }
   const double half = 0.5 * tot;
@@ -989,7 +996,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   int chu = -1, chv = -1, lastu = 0, lastv = 0;
   double lbu = 0.0, lbv = 0.0;
 #pragma unroll
-  for (int c = 0; c < WMF_NC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     if (chu < 0 && su[c] > 0.0) { lastu = c; lbu = pu; }
     if (chv < 0 && sv[c] > 0.0) { lastv = c; lbv = pv; }
     if (chu < 0 && pu + su[c] >= half) { chu = c; bu = pu; }
