@@ -87,6 +87,7 @@ KERNEL_BYTES_PER_PX = {
     # the pipelined SOR: one launch per solve, bytes counted per sweep done
     # ("sor_pipe.active" = sweeps x level pixels)
     "sor_pipe": 36 + 8 + 8,
+    "sor_wg": 36 + 8 + 8,  # the one-workgroup form of small levels (LDS ring), per sweep done
 }
 # VALU issue peak (MI355X_MICROARCH.md: a wave issues one VALU instruction per
 # 2 cycles per SIMD; 256 CUs x 4 SIMDs at 2.4 GHz): wave-instructions / s
@@ -111,6 +112,8 @@ def parse(argv=None):
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-stream", action="store_true", help="skip the streamed (pair pool) rate")
     ap.add_argument("--cpu-sample", type=int, default=360, help="crop height of the CPU-baseline sample")
+    ap.add_argument("--sor-pipeline", type=int, default=None,
+                    help="OF_OPT_SOR_PIPELINE for 'sor' (0 per sweep, 1 pipelined, 2 + one-workgroup small levels)")
     ap.add_argument("--rccl-self", action="store_true",
                     help="N = 1: one-rank RCCL communicator + the per-step gather in the timed loop "
                          "(the one-GPU proxy of the N > 1 timed path)")
@@ -455,11 +458,11 @@ def inner_loop_of(ktimes, per_level):
         elif name == "sor_sweep":
             byt += KERNEL_BYTES_PER_PX["sor_sweep"] * rec["px"]
             ms += rec["ms_total"]
-        elif name in ("pcg_iter", "sor_pipe"):
+        elif name in ("pcg_iter", "sor_pipe", "sor_wg"):
             ms += rec["ms_total"]
         elif name in INNER_TIME_ONLY:
             ms += rec["ms_total"]
-    for it in ("pcg_iter", "sor_pipe"):
+    for it in ("pcg_iter", "sor_pipe", "sor_wg"):
         act = ktimes.get(it + ".active")
         if act:
             byt += KERNEL_BYTES_PER_PX[it] * act["px"]
@@ -536,7 +539,7 @@ def level_breakdown(levels, per_level, pairs):
         rec = {"h": lv["h"], "w": lv["w"], "wall_ms": round(wall, 3), "kernel_ms": round(kern, 3),
                "gap_ms": round(wall - kern, 3), "gap_share": round((wall - kern) / wall, 4) if wall > 0 else None,
                "top": {n: round(v, 3) for n, v in sorted(ks.items(), key=lambda kv: -kv[1])[:4]}}
-        for solver in ("sor_pipe", "sor_sweep"):
+        for solver in ("sor_wg", "sor_pipe", "sor_sweep"):
             if (solver, px) in per_level:
                 sw = per_level.get((solver + ".active", px), per_level[(solver, px)])["px"] / px / pairs
                 ms = per_level[(solver, px)]["ms_total"] / pairs
@@ -596,6 +599,8 @@ def main(argv=None):
         return 0
     import_native()
     ctx = _native.Context(local)
+    if args.sor_pipeline is not None:
+        ctx.set_option(_abi.OF_OPT_SOR_PIPELINE, args.sor_pipeline)
     lib = ctx.lib
     H, W = args.height, args.width
     P0 = make_params(args)
@@ -719,6 +724,8 @@ def main(argv=None):
     streamed = None
     if not args.no_stream:
         sctx = _native.Context(local)
+        if args.sor_pipeline is not None:
+            sctx.set_option(_abi.OF_OPT_SOR_PIPELINE, args.sor_pipeline)
         slib = sctx.lib
         sctx.check(slib.of_pairs_open(sctx.handle, H, W, 3, C.byref(P0), args.lanes))
         souts = [[np.empty((2, H, W), dtype=np.float32) for _ in seeds] for _ in range(2)]

@@ -179,6 +179,10 @@ struct HostStage {
 #define OF_SOR_PIPE_WAVES 512
 #endif
 // dynamic LDS of a k_sor_pipe wave (unused): bounds the waves per CU
+// k_sor_wg's sweep ring in LDS (the rest of the 160 KB holds its stamps)
+#ifndef OF_SORW_RING_BYTES
+#define OF_SORW_RING_BYTES (144 * 1024)
+#endif
 #ifndef OF_SOR_PIPE_SHM
 #define OF_SOR_PIPE_SHM (32 * 1024)
 #endif
@@ -1126,7 +1130,45 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
   a.maxiter = P->sor_max_iters;
   HIPCHK(hipMemsetAsync(c->d_sor_sync, 0, OF_SOR_SYNC_BYTES, c->stream));
   launch(c, "sor_init", k_sor_init, dim3(std::min(1024, (H * b.P + 63) / 64)), dim3(64), 0, a);
-  if (c->opt_sor_pipe && a.maxiter > 0) {
+  // levels of <= 64 rows whose sweep ring fits in LDS (OF_OPT_SOR_PIPELINE 2):
+  // the pipelined solve in one workgroup, hand-offs through LDS (k_sor_wg)
+  if (c->opt_sor_pipe == 2 && a.maxiter > 0 && H <= 64) {
+    const size_t buf = sizeof(float2) * (size_t)H * W;
+    const int S = (int)std::min<size_t>(SORW_MAXW, OF_SORW_RING_BYTES / buf);
+    if (S >= 2) {
+      SorWgArgs w;
+      memset(&w, 0, sizeof(w));
+      w.coef = coef.p;
+      w.b = b.p;
+      w.x = x.p;
+      w.H = H;
+      w.W = W;
+      w.P = b.P;
+      w.ps = ps;
+      w.S = S;
+      w.nw = std::min(SORW_MAXW, 2 * S);
+      w.omega = (float)P->sor_omega;
+      w.tol = P->sor_tol;
+      w.maxiter = P->sor_max_iters;
+      w.st = c->d_state;
+      w.fail = a.fail;
+      launch(c, "sor_wg", k_sor_wg, dim3(1), dim3(64 * w.nw), buf * S + sizeof(SorWgShared), w);
+      HIPCHK(hipMemcpyAsync(&c->h_state[0], c->d_state, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_norm, a.fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      if (*(const int *)c->h_norm == 0) {
+        const PcgState &st = c->h_state[0];
+        REQUIRE(st.done != 0, OF_EHIP, "SOR workgroup solve ended without a decided sweep");
+        note_active(c, "sor_wg", st.iter, (double)H * W);
+        return {st.iter, st.done, st.xnorm2 > 0 ? std::sqrt(st.rr / st.xnorm2) : 0.0};
+      }
+      // a wait gave up: x and the state are k_sor_init's; the pipelined
+      // kernels below redo the solve (the same iterate)
+      ++c->sor_fallbacks;
+      HIPCHK(hipMemsetAsync(c->d_sor_sync, 0, OF_SOR_SYNC_BYTES, c->stream));
+    }
+  }
+  if (c->opt_sor_pipe >= 1 && a.maxiter > 0) {
     // ring of S sweep buffers: enough for the sweeps the persistent grid (one
     // wave per CU) can hold in flight, 2 * nstrips units per sweep
     const int S = std::max(4, std::min(SOR_RING_MAX, OF_SOR_PIPE_WAVES / (2 * nstrips) + 2));
@@ -2105,6 +2147,8 @@ int of_ctx_create(int device, of_ctx **out) {
     HIPCHK(hipMalloc(&c->d_rlog, sizeof(double) * 4 * OF_SLOG_MAX));
     HIPCHK(hipFuncSetAttribute((const void *)k_sor_lex, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_SHM));
     HIPCHK(hipFuncSetAttribute((const void *)k_sor_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, OF_SOR_PIPE_SHM));
+    HIPCHK(hipFuncSetAttribute((const void *)k_sor_wg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(OF_SORW_RING_BYTES + sizeof(SorWgShared))));
     HIPCHK(hipMalloc(&c->d_mm, sizeof(uint32_t) * 64));
     HIPCHK(hipMalloc(&c->d_norm, sizeof(double)));
     HIPCHK(hipHostMalloc(&c->h_norm, sizeof(double), hipHostMallocDefault));
@@ -2188,7 +2232,7 @@ int of_set_option(of_ctx *c, int option, int value) {
   REFUSE_WHILE_POOL(c)
   switch (option) {
     case OF_OPT_SOR_PIPELINE:
-      c->opt_sor_pipe = value ? 1 : 0;
+      c->opt_sor_pipe = value < 0 ? 0 : (value > 2 ? 2 : value);
       return OF_OK;
     case OF_OPT_FUSED_WARP:
       c->opt_fused_warp = value ? 1 : 0;

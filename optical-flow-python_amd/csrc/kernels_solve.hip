@@ -2195,6 +2195,242 @@ __global__ __launch_bounds__(256) void k_sor_pipe_final(SorPipeArgs a, float2 *x
 }
 
 // ---------------------------------------------------------------------------
+// k_sor_wg: the pipelined lexicographic SOR of a small level (<= 64 rows: one
+// strip per half) in ONE workgroup, with the sweep ring and the progress
+// stamps in LDS.  Same schedule as k_sor_pipe -- unit (sweep k, half) relaxes
+// the anti-diagonals of the strip, sweep k+1 trails sweep k, sweep k writes
+// ring slot k mod S and reads slot k-1 mod S, a slot is reused only after the
+// decision of the sweep that held it -- and the same relaxation operand for
+// operand (sor_relax), so the iterate and the sweep count are k_sor_lex's
+// bitwise.  What changes is the hand-off: in k_sor_pipe every unit is a wave
+// somewhere on the chip, and a sweep's rows reach the next sweep through L2
+// (sc1 stores, a stamp every SOR_G steps after s_waitcnt vmcnt(0), polled with
+// sc1 loads): ~1 us per hand-off, so at 30x40 a sweep costs ~27 us for ~70
+// relaxation steps.  Here the waves share one CU's LDS: a stamp is a ds_write
+// and a poll a ds_read.
+//
+// Units are static: wave w takes tickets w, w + nw, ... in order (ticket 2k =
+// (k, u), 2k + 1 = (k, v)); every wait is on a lower ticket (the u unit of
+// its sweep, the v unit of the previous sweep, the decision of sweep k - S),
+// and all waves of a workgroup are resident, so the lowest unfinished ticket
+// can always proceed: no deadlock.  Waits are bounded (fail) and end on an
+// earlier decision (stop), so every wave reaches the final barrier.
+#ifndef SORW_G
+#define SORW_G 2  // steps between progress stamps
+#endif
+#define SORW_MAXW 16
+struct SorWgArgs {
+  const float *coef;  // 7 planes, plane stride ps
+  const float2 *b;
+  float2 *x;          // the solution (pitched), written from the decided slot
+  int H, W, P;
+  size_t ps;
+  int S, nw;          // ring depth, waves
+  float omega;
+  double tol;
+  int maxiter;
+  PcgState *st;
+  int *fail;          // global: set when a wait gave up (the host reruns per sweep)
+};
+struct SorWgShared {  // LDS after the ring
+  int prog[SORW_MAXW + 2][2];  // [slot][half] progress stamps (sweep * stride + steps)
+  int dec[SORW_MAXW + 2];      // (sweep + 1) * 4 + done code, once decided
+  int cnt[SORW_MAXW + 2];      // finished units per slot (monotone)
+  double part[SORW_MAXW + 2][2][2];
+  double res[SORW_MAXW + 2][2];
+  int stop, fail;
+};
+__device__ __forceinline__ int sorw_ld(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void sorw_st(int *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wave-uniform wait until *p >= need; false when abandoned (an earlier sweep
+// decided, or a wait gave up)
+__device__ __forceinline__ bool sorw_wait(SorWgShared &sh, const int *p, int need, int &known, int k) {
+  for (int n = 0; known < need; ++n) {
+    known = __builtin_amdgcn_readfirstlane(sorw_ld(p));
+    if (known >= need) break;
+    if ((n & 15) == 15 &&
+        (__builtin_amdgcn_readfirstlane(sorw_ld(&sh.stop)) < k || __builtin_amdgcn_readfirstlane(sorw_ld(&sh.fail))))
+      return false;
+    if (n > (1 << 22)) {
+      if ((threadIdx.x & 63) == 0) sorw_st(&sh.fail, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+template <int PH>
+__device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *ring, SorWgShared &sh, int k, int stride,
+                                          double &dn, double &xn) {
+  const int lane = threadIdx.x & 63, H = a.H, W = a.W;
+  const bool rowok = lane < H;
+  const size_t ps = a.ps;
+  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
+  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
+  const size_t row = (size_t)(rowok ? lane : 0) * a.P;
+  const int lrow = (rowok ? lane : 0) * W;
+  const int nsteps = W + H - 1;  // lane H - 1 relaxes column W - 1 at step W + H - 2
+  const int S = a.S, cur = k % S, prv = (k + S - 1) % S;
+  float *xc = reinterpret_cast<float *>(ring + (size_t)cur * H * W);
+  const float2 *xp = ring + (size_t)prv * H * W;
+  const int base = k * stride, pbase = (k - 1) * stride;
+  int *my = &sh.prog[cur][PH];
+  const int *pu = &sh.prog[cur][0];    // (k, u)
+  const int *pold = &sh.prog[prv][1];  // (k - 1, v)
+  int known_u = 0, known_old = 0;
+  const float om = a.omega, om1 = 1.0f - a.omega;
+
+  // coefficients of column t + SOR_D - lane, SOR_D steps ahead (global, L2)
+  float WX[8], WY[8], DG[8], CC[8], BB[8];
+  auto fetch = [&](int t) {
+    const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
+    const bool ok = rowok && jp >= 0 && jp < W;
+    const size_t o = row + (ok ? jp : 0);
+    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
+    WY[q] = ok && lane + 1 < H ? wyp[o] : 0.f;
+    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
+    CC[q] = ok ? ccp[o] : 0.f;
+    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
+  };
+  // the old (and, for v, this sweep's u) values of column jn of this lane's row
+  auto xval = [&](int jn) {
+    if (!rowok || jn < 0 || jn >= W) return make_float2(0.f, 0.f);
+    const float2 o = k > 0 ? xp[lrow + jn] : make_float2(0.f, 0.f);
+    return PH ? make_float2(xc[2 * (lrow + jn)], o.y) : o;
+  };
+#pragma unroll
+  for (int t = -SOR_D; t < 0; ++t) fetch(t);
+  // column 0 - lane (the first step's point): needs (k, u) step 1 / (k-1, v)
+  // step 1
+  bool alive = true;
+  if (k > 0) alive = sorw_wait(sh, pold, pbase + 1, known_old, k);
+  if (PH == 1) alive = alive && sorw_wait(sh, pu, base + 1, known_u, k);
+  if (!alive) return false;
+  float2 Xq = xval(-lane);
+  float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
+  for (int t0 = 0; t0 < nsteps; t0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u;
+      if (t >= nsteps) break;
+      fetch(t);
+      // the next column (t + 1 - lane): relaxed by (k-1, v) at its step t + 1
+      // and (v half) by (k, u) at its step t + 1
+      const int need = min(t + 2, nsteps);
+      if (k > 0) alive = alive && sorw_wait(sh, pold, pbase + need, known_old, k);
+      if (PH == 1) alive = alive && sorw_wait(sh, pu, base + need, known_u, k);
+      if (!alive) return false;
+      const float2 Xn = xval(t + 1 - lane);
+      const int j = t - lane, q = t & 7;
+      const bool act = rowok && j >= 0 && j < W;
+      const float old = PH ? Xq.y : Xq.x, other = PH ? Xq.x : Xq.y;
+      const float right = PH ? Xn.y : Xn.x;
+      float down = sor_from_down(right);
+      float up = sor_from_up(res), wu = sor_from_up(wy_prev);
+      if (lane == 0) {  // no strip above
+        up = 0.f;
+        wu = 0.f;
+      }
+      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
+      if (act) {
+        xc[2 * (lrow + j) + PH] = nw;
+        sor_acc(nw, old, dn, xn);
+      } else {
+        nw = 0.f;
+      }
+      res = nw;
+      wx_prev = act ? WX[q] : 0.f;
+      wy_prev = act ? WY[q] : 0.f;
+      Xq = Xn;
+      if (((t + 1) % SORW_G) == 0 || t + 1 == nsteps) {
+        if (lane == 0) sorw_st(my, base + t + 1);
+      }
+    }
+  }
+  return alive;
+}
+
+__global__ __launch_bounds__(SORW_MAXW * 64) void k_sor_wg(SorWgArgs a) {
+  extern __shared__ double sorw_lds[];
+  float2 *ring = reinterpret_cast<float2 *>(sorw_lds);
+  SorWgShared &sh = *reinterpret_cast<SorWgShared *>(ring + (size_t)a.S * a.H * a.W);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int stride = a.W + a.H + 1;  // > steps of a unit
+  if (threadIdx.x < SORW_MAXW + 2) {
+    sh.prog[threadIdx.x][0] = sh.prog[threadIdx.x][1] = -1;
+    sh.dec[threadIdx.x] = 0;
+    sh.cnt[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) {
+    sh.stop = 0x7fffffff;
+    sh.fail = 0;
+  }
+  __syncthreads();
+  if (wave < a.nw) {
+    for (int tk = wave;; tk += a.nw) {
+      const int k = tk >> 1, ph = tk & 1;
+      if (k >= a.maxiter) break;
+      if (__builtin_amdgcn_readfirstlane(sorw_ld(&sh.stop)) < k || __builtin_amdgcn_readfirstlane(sorw_ld(&sh.fail)))
+        break;
+      const int cur = k % a.S;
+      if (k >= a.S) {
+        // slot `cur` still holds sweep k - S: wait for its decision; if it
+        // ended the solve, this and every later unit is void
+        int known = 0;
+        if (!sorw_wait(sh, &sh.dec[cur], (k - a.S + 1) * 4, known, k)) break;
+        if (known & 3) break;
+      }
+      double dn = 0.0, xn = 0.0;
+      const bool ok = ph ? sorw_unit<1>(a, ring, sh, k, stride, dn, xn) : sorw_unit<0>(a, ring, sh, k, stride, dn, xn);
+      if (!ok) break;
+      dn = wave_sum(dn);
+      xn = wave_sum(xn);
+      if (lane == 0) {
+        sh.part[cur][ph][0] = dn;
+        sh.part[cur][ph][1] = xn;
+        const int c = __hip_atomic_fetch_add(&sh.cnt[cur], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) + 1;
+        if (c == (k / a.S + 1) * 2) {
+          // the last unit of sweep k: its stopping test, k_sor_lex's order
+          double sd = 0.0, sx = 0.0;
+          for (int b = 0; b < 2; ++b) {
+            sd += sh.part[cur][b][0];
+            sx += sh.part[cur][b][1];
+          }
+          const int done = sqrt(sd) < a.tol * sqrt(sx) ? 1 : (k + 1 >= a.maxiter ? 2 : 0);
+          sh.res[cur][0] = sd;
+          sh.res[cur][1] = sx;
+          if (done) __hip_atomic_fetch_min(&sh.stop, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+          sorw_st(&sh.dec[cur], (k + 1) * 4 + done);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int K = sh.stop;
+  if (sh.fail || K == 0x7fffffff) {
+    if (threadIdx.x == 0) __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int cur = K % a.S;
+  const float2 *src = ring + (size_t)cur * a.H * a.W;
+  for (int e = threadIdx.x; e < a.H * a.W; e += blockDim.x) {
+    const int i = e / a.W, j = e - i * a.W;
+    a.x[(size_t)i * a.P + j] = src[e];
+  }
+  if (threadIdx.x == 0) {
+    a.st->iter = K + 1;
+    a.st->rr = sh.res[cur][0];
+    a.st->xnorm2 = sh.res[cur][1];
+    a.st->done = sh.dec[cur] & 3;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // sum of squares of a float2 field (HS early exit ||x||_2 < 1e-3, hs.py:127):
 // partials then a one-block finish
 __global__ __launch_bounds__(256) void k_norm2_part(const float2 *__restrict__ x, int H, int W, int P, double *part) {

@@ -233,6 +233,68 @@ def test_sor_pipelined_bitwise_e2e(golden):
     np.testing.assert_array_equal(uv1, uv0)
 
 
+def _sor_modes(fn, modes=(0, 2)):
+    """fn() under each OF_OPT_SOR_PIPELINE mode (0 per sweep, 1 pipelined,
+    2 pipelined + the one-workgroup LDS kernel for levels of <= 64 rows);
+    returns the results and, per mode, the kernel names that ran."""
+    import ctypes as C
+    from optical_flow import _native as nat
+    from optical_flow._abi import OF_OPT_SOR_PIPELINE
+    ctx = nat.context()
+    out, ran = [], []
+    try:
+        for m in modes:
+            ctx.set_option(OF_OPT_SOR_PIPELINE, m)
+            ctx.check(ctx.lib.of_set_profiling(ctx.handle, 1))
+            out.append(fn())
+            n = C.c_int(0)
+            names = (C.c_char_p * 256)()
+            ctx.check(ctx.lib.of_kernel_times(ctx.handle, 256, names, None, None, None, C.byref(n)))
+            ran.append({names[i].decode() for i in range(min(n.value, 256))})
+            ctx.check(ctx.lib.of_set_profiling(ctx.handle, 0))
+    finally:
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
+    return out, ran
+
+
+@pytest.mark.parametrize("H,W,maxit", [(40, 56, 10000), (64, 64, 10000), (30, 40, 10000), (60, 80, 10000),
+                                       (17, 30, 10000), (5, 300, 10000), (30, 40, 7), (60, 80, 1), (64, 200, 10000)])
+def test_sor_workgroup_bitwise(H, W, maxit):
+    """k_sor_wg (a level of <= 64 rows solved in one workgroup, sweep ring and
+    progress stamps in LDS) gives the same iterate and sweep count bitwise as
+    k_sor_lex, including the sweep limit; 64x200 needs more LDS than the ring
+    may take and stays on k_sor_pipe."""
+    from optical_flow import _abi, _native as nat
+    from optical_flow.methods.config import load_of_method
+    A, b = _spd_flow_system(H, W, seed=13 * H + W)
+    o = load_of_method("hs")
+    o.solver = "sor"
+    o.sor_max_iters = maxit
+
+    def run():
+        x = o._solve_linear_system(A, b, (H, W, 2))
+        return x, dict(o.last_solve)
+    fb0 = nat.context().get_option(_abi.OF_OPT_SOR_FALLBACKS)
+    ((x0, s0), (x2, s2)), (r0, r2) = _sor_modes(run)
+    assert nat.context().get_option(_abi.OF_OPT_SOR_FALLBACKS) == fb0
+    assert s2["iters"] == s0["iters"] and s2.get("done") == s0.get("done"), (s2, s0)
+    if maxit < 10000:
+        assert s2["iters"] == maxit
+    np.testing.assert_array_equal(x2, x0)
+    assert "sor_sweep" in r0
+    assert ("sor_wg" in r2) == (H * W * 8 * 2 <= 144 * 1024), r2
+
+
+def test_sor_workgroup_bitwise_e2e(golden):
+    """HS with 'sor' end to end with the one-workgroup kernel on its small
+    levels: the flow equals the per-sweep kernel's bitwise."""
+    import optical_flow
+    d = golden("e2e_synth.npz")
+    (uv0, uv2), (r0, r2) = _sor_modes(lambda: optical_flow.estimate_flow(d["im1"], d["im2"], "hs", {"solver": "sor"}))
+    assert "sor_wg" in r2
+    np.testing.assert_array_equal(uv2, uv0)
+
+
 def test_sor_device_memory_flat(golden):
     """the pipelined SOR's ring of sweep buffers is one grow-only
     buffer per context (was carved from the per-pair arena on every solve:

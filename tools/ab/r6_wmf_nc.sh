@@ -20,4 +20,6 @@ for rep in 1 2; do for L in $A $B; do
   OPTFLOW_LIB=$L tools/gpu_step.sh 200 $O/bench_tmp.log python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-profile --no-stream || exit $?
   grep '^{' $O/bench_tmp.log >> $O/bench_ab.log
 done; done
-tools/gpu_step.sh 300 $O/bench_cfg2.log python -u bench.py --method hs --solver sor --height 480 --width 640 --no-cpu-baseline
+tools/gpu_step.sh 300 $O/bench_cfg2.log python -u bench.py --method hs --solver sor --height 480 --width 640 --no-cpu-baseline && \
+tools/gpu_step.sh 300 $O/sor_tests.log python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_stages.py -k "sor" && \
+tools/gpu_step.sh 300 $O/bench_cfg2_wg.log python -u bench.py --method hs --solver sor --height 480 --width 640 --no-cpu-baseline --sor-pipeline 2
