@@ -2218,7 +2218,9 @@ __global__ __launch_bounds__(256) void k_sor_pipe_final(SorPipeArgs a, float2 *x
 #ifndef SORW_G
 #define SORW_G 2  // steps between progress stamps
 #endif
-#define SORW_MAXW 16
+// waves per workgroup: 8 (2 per SIMD) keep the unit's prefetch ring and both
+// halves' code in registers (a 16-wave build has 128 VGPRs and spills)
+#define SORW_MAXW 8
 struct SorWgArgs {
   const float *coef;  // 7 planes, plane stride ps
   const float2 *b;
@@ -2240,11 +2242,25 @@ struct SorWgShared {  // LDS after the ring
   double res[SORW_MAXW + 2][2];
   int stop, fail;
 };
+// LDS stamps without acquire / release: at workgroup scope those also wait
+// for the wave's outstanding global loads (s_waitcnt vmcnt(0)), i.e. for the
+// coefficient prefetch SOR_D steps ahead, every step (1.5 us per step
+// measured), and so does an inline-asm wait with a memory clobber.  Not
+// needed: the LDS executes a CU's DS instructions in order, so a unit's data
+// ds_writes land before its later stamp ds_write, and a reader's data
+// ds_reads (issued after the stamp value they depend on returned) see them.
+// Only the compiler must keep LDS accesses on their side of a stamp access:
+// signal fences (no instruction).
 __device__ __forceinline__ int sorw_ld(const int *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  return v;
 }
 __device__ __forceinline__ void sorw_st(int *p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 // wave-uniform wait until *p >= need; false when abandoned (an earlier sweep
 // decided, or a wait gave up)
@@ -2264,14 +2280,29 @@ __device__ __forceinline__ bool sorw_wait(SorWgShared &sh, const int *p, int nee
   return true;
 }
 
+// the dynamic LDS of k_sor_wg: [S][H][W] float2 sweep ring, then
+// SorWgShared, addressed from the symbol (LDS instructions, not flat ones:
+// a flat access counts in both vmcnt and lgkmcnt, so waiting for it would
+// also wait for the global coefficient prefetch)
+extern __shared__ double sorw_lds[];
+__device__ __forceinline__ float2 *sorw_ring() { return reinterpret_cast<float2 *>(sorw_lds); }
+__device__ __forceinline__ SorWgShared &sorw_sh(const SorWgArgs &a) {
+  return *reinterpret_cast<SorWgShared *>(sorw_ring() + (size_t)a.S * a.H * a.W);
+}
+
 template <int PH>
-__device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *ring, SorWgShared &sh, int k, int stride,
-                                          double &dn, double &xn) {
+__device__ __forceinline__ bool sorw_unit(const SorWgArgs &a, int k, int stride, double &dn, double &xn) {
+  float2 *ring = sorw_ring();
+  SorWgShared &sh = sorw_sh(a);
   const int lane = threadIdx.x & 63, H = a.H, W = a.W;
   const bool rowok = lane < H;
   const size_t ps = a.ps;
-  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
-  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
+  // global (not generic) pointers: global_load, counted in vmcnt only
+  typedef const __attribute__((address_space(1))) float gf;
+  gf *cf = (gf *)a.coef;
+  gf *bp = (gf *)a.b + PH;  // b's component of this half (float2 planes)
+  gf *wxp = cf + (PH ? 2 : 0) * ps, *wyp = cf + (PH ? 3 : 1) * ps;
+  gf *dgp = cf + (PH ? 6 : 4) * ps, *ccp = cf + 5 * ps;
   const size_t row = (size_t)(rowok ? lane : 0) * a.P;
   const int lrow = (rowok ? lane : 0) * W;
   const int nsteps = W + H - 1;  // lane H - 1 relaxes column W - 1 at step W + H - 2
@@ -2287,21 +2318,34 @@ __device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *
 
   // coefficients of column t + SOR_D - lane, SOR_D steps ahead (global, L2)
   float WX[8], WY[8], DG[8], CC[8], BB[8];
+  // every load unconditional at a clamped address, the value selected after
+  // it: loads under a branch make the compiler wait for all of them
+  // (vmcnt(0)) at every step instead of for the one SOR_D steps old
+  // The raw values go into the ring and are masked at the step that uses
+  // them (+0 where the reference has no entry), by an AND the compiler cannot
+  // see through: a mask or select it can see becomes a masked load, whose
+  // value is then waited for at once (vmcnt(0)) instead of SOR_D steps later
+  auto keep = [](float v, bool c) {
+    float r;
+    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(0u - (unsigned)c));
+    return r;
+  };
   auto fetch = [&](int t) {
     const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
-    const bool ok = rowok && jp >= 0 && jp < W;
-    const size_t o = row + (ok ? jp : 0);
-    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
-    WY[q] = ok && lane + 1 < H ? wyp[o] : 0.f;
-    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
-    CC[q] = ok ? ccp[o] : 0.f;
-    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
+    const size_t o = row + min(max(jp, 0), W - 1);
+    WX[q] = wxp[o];
+    WY[q] = wyp[o];
+    DG[q] = dgp[o];
+    CC[q] = ccp[o];
+    BB[q] = bp[2 * o];
   };
   // the old (and, for v, this sweep's u) values of column jn of this lane's row
   auto xval = [&](int jn) {
-    if (!rowok || jn < 0 || jn >= W) return make_float2(0.f, 0.f);
-    const float2 o = k > 0 ? xp[lrow + jn] : make_float2(0.f, 0.f);
-    return PH ? make_float2(xc[2 * (lrow + jn)], o.y) : o;
+    const bool ok = rowok && jn >= 0 && jn < W;
+    const int e = lrow + min(max(jn, 0), W - 1);
+    const float2 o = xp[e];
+    const float u = PH ? xc[2 * e] : o.x;
+    return make_float2(keep(u, ok && (PH || k > 0)), keep(o.y, ok && k > 0));
   };
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
@@ -2328,6 +2372,8 @@ __device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *
       const float2 Xn = xval(t + 1 - lane);
       const int j = t - lane, q = t & 7;
       const bool act = rowok && j >= 0 && j < W;
+      const float wxq = keep(WX[q], act && j + 1 < W), wyq = keep(WY[q], act && lane + 1 < H);
+      const float dgq = keep(sor_dg(DG[q]), act), ccq = keep(CC[q], act), bbq = keep(BB[q], act);
       const float old = PH ? Xq.y : Xq.x, other = PH ? Xq.x : Xq.y;
       const float right = PH ? Xn.y : Xn.x;
       float down = sor_from_down(right);
@@ -2336,7 +2382,7 @@ __device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *
         up = 0.f;
         wu = 0.f;
       }
-      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
+      float nw = sor_relax(bbq, wx_prev, res, wxq, right, wyq, down, wu, up, ccq, other, dgq, old, om, om1);
       if (act) {
         xc[2 * (lrow + j) + PH] = nw;
         sor_acc(nw, old, dn, xn);
@@ -2344,8 +2390,8 @@ __device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *
         nw = 0.f;
       }
       res = nw;
-      wx_prev = act ? WX[q] : 0.f;
-      wy_prev = act ? WY[q] : 0.f;
+      wx_prev = wxq;
+      wy_prev = wyq;
       Xq = Xn;
       if (((t + 1) % SORW_G) == 0 || t + 1 == nsteps) {
         if (lane == 0) sorw_st(my, base + t + 1);
@@ -2356,9 +2402,8 @@ __device__ __attribute__((noinline)) bool sorw_unit(const SorWgArgs &a, float2 *
 }
 
 __global__ __launch_bounds__(SORW_MAXW * 64) void k_sor_wg(SorWgArgs a) {
-  extern __shared__ double sorw_lds[];
-  float2 *ring = reinterpret_cast<float2 *>(sorw_lds);
-  SorWgShared &sh = *reinterpret_cast<SorWgShared *>(ring + (size_t)a.S * a.H * a.W);
+  float2 *ring = sorw_ring();
+  SorWgShared &sh = sorw_sh(a);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int stride = a.W + a.H + 1;  // > steps of a unit
   if (threadIdx.x < SORW_MAXW + 2) {
@@ -2386,7 +2431,7 @@ __global__ __launch_bounds__(SORW_MAXW * 64) void k_sor_wg(SorWgArgs a) {
         if (known & 3) break;
       }
       double dn = 0.0, xn = 0.0;
-      const bool ok = ph ? sorw_unit<1>(a, ring, sh, k, stride, dn, xn) : sorw_unit<0>(a, ring, sh, k, stride, dn, xn);
+      const bool ok = ph ? sorw_unit<1>(a, k, stride, dn, xn) : sorw_unit<0>(a, k, stride, dn, xn);
       if (!ok) break;
       dn = wave_sum(dn);
       xn = wave_sum(xn);
