@@ -1757,6 +1757,14 @@ __device__ __forceinline__ float sor_relax(float bb, float wl, float left, float
   return fabsf(dg) < 1e-15f ? old : fmaf(om1, old, (om * sgm) / dg);
 #endif
 }
+// v & (c ? ~0 : 0), opaque to the compiler (see the SOR prefetch rings)
+__device__ __forceinline__ float sorw_keep(float v, bool c) {
+  float r;
+  asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(0u - (unsigned)c));
+  return r;
+}
+// global (not generic) float pointers: global_load, counted in vmcnt only
+typedef const __attribute__((address_space(1))) float sorw_gf;
 // the diagonal as sor_relax takes it
 __device__ __forceinline__ float sor_dg(float a) {
 #if SOR_RCP
@@ -2026,8 +2034,9 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   const int i0 = s * 64, i = i0 + lane;
   const bool rowok = i < H;
   const size_t ps = a.ps;
-  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
-  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
+  sorw_gf *gcf = (sorw_gf *)a.coef;
+  sorw_gf *gwxp = gcf + (PH ? 2 : 0) * ps, *gwyp = gcf + (PH ? 3 : 1) * ps;
+  sorw_gf *gdgp = gcf + (PH ? 6 : 4) * ps, *gccp = gcf + 5 * ps, *gbp = (sorw_gf *)a.b + PH;
   const size_t row = (size_t)(rowok ? i : 0) * P;
   const bool has_up = s > 0, has_dn = i0 + 64 < H;
   const size_t row_up = (size_t)(has_up ? i0 - 1 : 0) * P, row_dn = (size_t)(has_dn ? i0 + 64 : 0) * P;
@@ -2047,7 +2056,13 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   const float om = a.omega, om1 = 1.0f - a.omega;
   bool alive = true;
 
-  float2 X[8], XU[8], XD[8];
+  // Prefetch ring: raw values loaded unconditionally at clamped addresses,
+  // masked (+0 where the reference has no entry) at the step that uses them
+  // by an AND the compiler cannot see through (sorw_keep): a select it can
+  // see turns into a masked load whose value is waited for at once
+  // (s_waitcnt vmcnt(0): the whole prefetch drained every step).  The row
+  // above / below (lanes 0 / 63 only) is one address for the whole wave.
+  float X0[8], X1[8], XU[8], XD[8];
   float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
   auto fetch = [&](int t) {  // column t + SOR_D - lane
     const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
@@ -2056,25 +2071,19 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
     if (k > 0 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pold, pbase + tp + 1, known_old, k);
     if (k > 0 && has_dn && tp - 63 >= 0 && tp - 63 < W)
       alive = alive && sorp_wait(a, pdn, pbase + tp - 62, known_dn, k);
-    const bool ok = rowok && jp >= 0 && jp < W;
-    const size_t o = row + (ok ? jp : 0);
-    if (PH == 0) X[q] = ok ? sor_ld(xp + o) : make_float2(0.f, 0.f);
-    else X[q] = ok ? make_float2(sor_ld1((const float *)(xc + o)), sor_ld1((const float *)(xp + o) + 1))
-                   : make_float2(0.f, 0.f);
-    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
-    WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
-    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
-    CC[q] = ok ? ccp[o] : 0.f;
-    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
-    if (lane == 0) {
-      const bool u = has_up && jp >= 0 && jp < W;
-      XU[q] = u ? sor_ld(xc + row_up + jp) : make_float2(0.f, 0.f);
-      WYU[q] = u ? wyp[row_up + jp] : 0.f;
-    }
-    if (lane == 63) {
-      const bool d = has_dn && jp >= 0 && jp < W;
-      XD[q] = d ? sor_ld(xp + row_dn + jp) : make_float2(0.f, 0.f);
-    }
+    const size_t o = row + min(max(jp, 0), W - 1);
+    const float *xo = (const float *)(PH ? xc + o : xp + o);
+    X0[q] = sor_ld1(xo);
+    X1[q] = sor_ld1((const float *)(xp + o) + 1);
+    WX[q] = gwxp[o];
+    WY[q] = gwyp[o];
+    DG[q] = gdgp[o];
+    CC[q] = gccp[o];
+    BB[q] = gbp[2 * o];
+    const int ju = min(max(tp, 0), W - 1), jd = min(max(tp - 63, 0), W - 1);
+    XU[q] = sor_ld1((const float *)(xc + row_up + ju) + PH);
+    WYU[q] = gwyp[row_up + ju];
+    XD[q] = sor_ld1((const float *)(xp + row_dn + jd) + PH);
   };
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
@@ -2089,18 +2098,22 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
       if (t >= nsteps) break;
       fetch(t);
       const int j = t - lane, q = t & 7, q1 = (t + 1) & 7;
-      const bool act = rowok && j >= 0 && j < W;
-      const float2 xo = X[q];
-      const float old = PH ? xo.y : xo.x, other = PH ? xo.x : xo.y;
-      const float right = PH ? X[q1].y : X[q1].x;
+      const bool act = rowok && j >= 0 && j < W, act1 = rowok && j + 1 >= 0 && j + 1 < W;
+      // X0 / X1: this half's component / the other one (PH 0: u, v; PH 1: v
+      // of the previous sweep in X1 and this sweep's u in X0)
+      const float old = sorw_keep(PH ? X1[q] : X0[q], act), other = sorw_keep(PH ? X0[q] : X1[q], act);
+      const float right = sorw_keep(PH ? X1[q1] : X0[q1], act1);
+      const float wxq = sorw_keep(WX[q], act && j + 1 < W), wyq = sorw_keep(WY[q], act && i + 1 < H);
+      const float dgq = sorw_keep(sor_dg(DG[q]), act), ccq = sorw_keep(CC[q], act), bbq = sorw_keep(BB[q], act);
       float down = sor_from_down(right);
-      if (lane == 63) down = PH ? XD[q].y : XD[q].x;
+      if (lane == 63) down = sorw_keep(XD[q], has_dn && j >= 0 && j < W);
       float up = sor_from_up(res), wu = sor_from_up(wy_prev);
       if (lane == 0) {
-        up = PH ? XU[q].y : XU[q].x;
-        wu = WYU[q];
+        const bool u = has_up && j >= 0 && j < W;
+        up = sorw_keep(XU[q], u);
+        wu = sorw_keep(WYU[q], u);
       }
-      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
+      float nw = sor_relax(bbq, wx_prev, res, wxq, right, wyq, down, wu, up, ccq, other, dgq, old, om, om1);
       if (act) {
         const size_t o = row + j;
         sor_st(xc + o, PH ? make_float2(other, nw) : make_float2(nw, other));
@@ -2109,8 +2122,8 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
         nw = 0.f;
       }
       res = nw;
-      wx_prev = act ? WX[q] : 0.f;
-      wy_prev = act ? WY[q] : 0.f;
+      wx_prev = wxq;
+      wy_prev = wyq;
       if (((t + 1) & (SOR_G - 1)) == 0 || t + 1 == nsteps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(my, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
