@@ -2064,8 +2064,22 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   // above / below (lanes 0 / 63 only) is one address for the whole wave.
   float X0[8], X1[8], XU[8], XD[8];
   float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
+  // Stale stamps: a poll is a global load, and waiting for its value waits
+  // for every load issued before it (vmcnt counts in order) -- the whole
+  // prefetch, at every poll.  So each step also loads the four stamps it may
+  // wait on into a ring, and the step 8 later first takes those values (by
+  // then returned: reading them waits for nothing newer) as lower bounds of
+  // the producers' progress (stamps only grow); it polls only when they do
+  // not cover what it needs.
+  int SUP[8], SU[8], SOLD[8], SDN[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) SUP[r] = SU[r] = SOLD[r] = SDN[r] = 0;
   auto fetch = [&](int t) {  // column t + SOR_D - lane
     const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
+    known_up = max(known_up, __builtin_amdgcn_readfirstlane(SUP[q]));
+    known_u = max(known_u, __builtin_amdgcn_readfirstlane(SU[q]));
+    known_old = max(known_old, __builtin_amdgcn_readfirstlane(SOLD[q]));
+    known_dn = max(known_dn, __builtin_amdgcn_readfirstlane(SDN[q]));
     if (has_up && tp >= 0 && tp < W) alive = alive && sorp_wait(a, pup, base + tp + 64, known_up, k);
     if (PH == 1 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pu, base + tp + 1, known_u, k);
     if (k > 0 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pold, pbase + tp + 1, known_old, k);
@@ -2084,6 +2098,10 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
     XU[q] = sor_ld1((const float *)(xc + row_up + ju) + PH);
     WYU[q] = gwyp[row_up + ju];
     XD[q] = sor_ld1((const float *)(xp + row_dn + jd) + PH);
+    SUP[q] = sor_poll(pup);
+    SU[q] = sor_poll(pu);
+    SOLD[q] = sor_poll(pold);
+    SDN[q] = sor_poll(pdn);
   };
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
