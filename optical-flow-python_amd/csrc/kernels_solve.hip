@@ -2064,27 +2064,22 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   // above / below (lanes 0 / 63 only) is one address for the whole wave.
   float X0[8], X1[8], XU[8], XD[8];
   float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
-  // Stale stamps: a poll is a global load, and waiting for its value waits
-  // for every load issued before it (vmcnt counts in order) -- the whole
-  // prefetch, at every poll.  So each step also loads the four stamps it may
-  // wait on into a ring, and the step 8 later first takes those values (by
-  // then returned: reading them waits for nothing newer) as lower bounds of
-  // the producers' progress (stamps only grow); it polls only when they do
-  // not cover what it needs.
-  int SUP[8], SU[8], SOLD[8], SDN[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) SUP[r] = SU[r] = SOLD[r] = SDN[r] = 0;
-  auto fetch = [&](int t) {  // column t + SOR_D - lane
+  // The hand-off waits of a group of 8 steps' fetches (columns tp = t +
+  // SOR_D - lane for t in [t_lo, t_hi]) at once, before the group: a wait
+  // inside every step made each step ~650 instructions of control flow, and
+  // a poll (a global load) waits for every load issued before it.  Each wait
+  // is the per-column one of the largest column the group needs.
+  auto group_wait = [&](int t_lo, int t_hi) {
+    const int lo = t_lo + SOR_D, hi = t_hi + SOR_D;
+    const int a0 = max(lo, 0), bw = min(hi, W - 1), bn = min(hi, nsteps - 1);
+    if (has_up && a0 <= bw) alive = alive && sorp_wait(a, pup, base + bw + 64, known_up, k);
+    if (PH == 1 && a0 <= bn) alive = alive && sorp_wait(a, pu, base + bn + 1, known_u, k);
+    if (k > 0 && a0 <= bn) alive = alive && sorp_wait(a, pold, pbase + bn + 1, known_old, k);
+    const int d0 = max(lo - 63, 0), d1 = min(hi - 63, W - 1);
+    if (k > 0 && has_dn && d0 <= d1) alive = alive && sorp_wait(a, pdn, pbase + d1 + 1, known_dn, k);
+  };
+  auto fetch = [&](int t) {  // column t + SOR_D - lane (after group_wait)
     const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
-    known_up = max(known_up, __builtin_amdgcn_readfirstlane(SUP[q]));
-    known_u = max(known_u, __builtin_amdgcn_readfirstlane(SU[q]));
-    known_old = max(known_old, __builtin_amdgcn_readfirstlane(SOLD[q]));
-    known_dn = max(known_dn, __builtin_amdgcn_readfirstlane(SDN[q]));
-    if (has_up && tp >= 0 && tp < W) alive = alive && sorp_wait(a, pup, base + tp + 64, known_up, k);
-    if (PH == 1 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pu, base + tp + 1, known_u, k);
-    if (k > 0 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pold, pbase + tp + 1, known_old, k);
-    if (k > 0 && has_dn && tp - 63 >= 0 && tp - 63 < W)
-      alive = alive && sorp_wait(a, pdn, pbase + tp - 62, known_dn, k);
     const size_t o = row + min(max(jp, 0), W - 1);
     const float *xo = (const float *)(PH ? xc + o : xp + o);
     X0[q] = sor_ld1(xo);
@@ -2098,22 +2093,22 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
     XU[q] = sor_ld1((const float *)(xc + row_up + ju) + PH);
     WYU[q] = gwyp[row_up + ju];
     XD[q] = sor_ld1((const float *)(xp + row_dn + jd) + PH);
-    SUP[q] = sor_poll(pup);
-    SU[q] = sor_poll(pu);
-    SOLD[q] = sor_poll(pold);
-    SDN[q] = sor_poll(pdn);
   };
+  group_wait(-SOR_D, -1);
+  if (!alive) return false;
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
-  if (!alive) return false;
 
   int stop_seen = 0x7fffffff;
   float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
+  // whole groups of 8 steps: the steps past nsteps relax nothing (every
+  // lane's column is past W) and store nothing
   for (int t0 = 0; t0 < nsteps; t0 += 8) {
+    group_wait(t0, t0 + 7);
+    if (!alive) return false;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = t0 + u;
-      if (t >= nsteps) break;
       fetch(t);
       const int j = t - lane, q = t & 7, q1 = (t + 1) & 7;
       const bool act = rowok && j >= 0 && j < W, act1 = rowok && j + 1 >= 0 && j + 1 < W;
@@ -2142,15 +2137,14 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
       res = nw;
       wx_prev = wxq;
       wy_prev = wyq;
-      if (((t + 1) & (SOR_G - 1)) == 0 || t + 1 == nsteps) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(my, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // *stop as read at the previous publication (its load had a whole
-        // publication interval to return): abandon a sweep past the answer
-        if (stop_seen < k || !alive) return false;
-        stop_seen = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
-      }
     }
+    // publish the group (its sc1 stores drained first)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(my, base + min(t0 + 8, nsteps), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // *stop as read at the previous publication (its load had a whole
+    // publication interval to return): abandon a sweep past the answer
+    if (stop_seen < k) return false;
+    stop_seen = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
   }
   return alive;
 }
@@ -2246,9 +2240,6 @@ __global__ __launch_bounds__(256) void k_sor_pipe_final(SorPipeArgs a, float2 *x
 // and all waves of a workgroup are resident, so the lowest unfinished ticket
 // can always proceed: no deadlock.  Waits are bounded (fail) and end on an
 // earlier decision (stop), so every wave reaches the final barrier.
-#ifndef SORW_G
-#define SORW_G 2  // steps between progress stamps
-#endif
 // waves per workgroup: 8 (2 per SIMD) keep the unit's prefetch ring and both
 // halves' code in registers (a 16-wave build has 128 VGPRs and spills)
 #define SORW_MAXW 8
@@ -2380,26 +2371,29 @@ __device__ __forceinline__ bool sorw_unit(const SorWgArgs &a, int k, int stride,
   };
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
-  // column 0 - lane (the first step's point): needs (k, u) step 1 / (k-1, v)
-  // step 1
+  // The waits of a group of 8 steps at once, before the group (a wait in
+  // every step made each step ~650 instructions of control flow): step t
+  // reads column t + 1 - lane, relaxed by (k-1, v) and (v half) by (k, u) at
+  // their step t + 1, so the group [t0, t0 + 7] needs their progress t0 + 9.
   bool alive = true;
-  if (k > 0) alive = sorw_wait(sh, pold, pbase + 1, known_old, k);
-  if (PH == 1) alive = alive && sorw_wait(sh, pu, base + 1, known_u, k);
+  auto group_wait = [&](int t0) {
+    const int need = min(t0 + 9, nsteps);
+    if (k > 0) alive = alive && sorw_wait(sh, pold, pbase + need, known_old, k);
+    if (PH == 1) alive = alive && sorw_wait(sh, pu, base + need, known_u, k);
+  };
+  group_wait(0);
   if (!alive) return false;
   float2 Xq = xval(-lane);
   float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
+  // whole groups: the steps past nsteps relax nothing (every lane's column
+  // is past W) and store nothing
   for (int t0 = 0; t0 < nsteps; t0 += 8) {
+    group_wait(t0);
+    if (!alive) return false;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = t0 + u;
-      if (t >= nsteps) break;
       fetch(t);
-      // the next column (t + 1 - lane): relaxed by (k-1, v) at its step t + 1
-      // and (v half) by (k, u) at its step t + 1
-      const int need = min(t + 2, nsteps);
-      if (k > 0) alive = alive && sorw_wait(sh, pold, pbase + need, known_old, k);
-      if (PH == 1) alive = alive && sorw_wait(sh, pu, base + need, known_u, k);
-      if (!alive) return false;
       const float2 Xn = xval(t + 1 - lane);
       const int j = t - lane, q = t & 7;
       const bool act = rowok && j >= 0 && j < W;
@@ -2424,10 +2418,8 @@ __device__ __forceinline__ bool sorw_unit(const SorWgArgs &a, int k, int stride,
       wx_prev = wxq;
       wy_prev = wyq;
       Xq = Xn;
-      if (((t + 1) % SORW_G) == 0 || t + 1 == nsteps) {
-        if (lane == 0) sorw_st(my, base + t + 1);
-      }
     }
+    if (lane == 0) sorw_st(my, base + min(t0 + 8, nsteps));
   }
   return alive;
 }
