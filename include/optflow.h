@@ -168,14 +168,19 @@ int of_synchronize(of_ctx *ctx);
 int of_set_profiling(of_ctx *ctx, int enable);
 /* solver options of a context (inherited by its batch lanes):
  *   OF_OPT_SOR_PIPELINE  1 (default): 'sor' runs its sweeps pipelined in one
- *                        persistent launch (k_sor_pipe); 0: one launch per
- *                        sweep (k_sor_lex).  Both give the same iterate and
- *                        sweep count bitwise. */
+ *                        persistent launch (k_sor_pipe); 2: as 1, and levels
+ *                        of <= 64 rows whose sweep ring fits in LDS run in
+ *                        one workgroup (k_sor_wg); 0: one launch per sweep
+ *                        (k_sor_lex).  All give the same iterate and sweep
+ *                        count bitwise. */
 #define OF_OPT_SOR_PIPELINE 1
 /*   OF_OPT_FUSED_WARP    1 (default): each warping iteration's partial_deriv
  *                        and flow_operator run as one kernel (no It / Ix /
  *                        Iy planes; 1 or 3 channels, one linearisation per
- *                        warp); 0: two kernels.  The same system either way
+ *                        warp); 0: two kernels.  The same system up to fp32
+ *                        rounding: the compiler contracts different products
+ *                        into fma in the two forms, so the planes agree to
+ *                        the family tolerance, not bitwise
  *                        (tests/test_gpu_stages.py). */
 #define OF_OPT_FUSED_WARP 3
 int of_set_option(of_ctx *ctx, int option, int value);

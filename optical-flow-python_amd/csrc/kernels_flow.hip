@@ -280,7 +280,9 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
 // Warp + derivatives + assembly in one pass: the
 // per-channel It / Ix / Iy of a pixel stay in registers, so the 24 B/px
 // round trip of the three planes (nc = 1) and one launch per warping
-// iteration go away.  Same arithmetic as k_partial_deriv + k_flow_operator.
+// iteration go away.  The same formulas as k_partial_deriv + k_flow_operator;
+// the compiler contracts different products into fma in the two forms, so
+// the planes agree to fp32 rounding (tests/test_gpu_stages.py), not bitwise.
 template <int INTERP, int NC, int M>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_warp_operator(DerivArgs d, OpArgs o, const float2 *__restrict__ uv,
                                                                 int H, int W, int P, size_t ps,

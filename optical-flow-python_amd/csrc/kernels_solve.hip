@@ -260,6 +260,30 @@ __device__ __forceinline__ cg_f4 cg_minv(const CgInv &m, cg_f4 r) {
 }
 __device__ __forceinline__ float cg_dot(cg_f4 a, cg_f4 b) { return a.x * b.x + a.y * b.y + (a.z * b.z + a.w * b.w); }
 
+// The lane's fixed-order partial sums of the 5 arrays of a 256-thread block
+// (nb <= PCG_MAX_BLOCKS: at most PCG_MAX_BLOCKS / 256 terms per lane), every
+// load issued before the first add.  A loop per array (the earlier form)
+// waited for each array's loads before issuing the next array's: five memory
+// round trips per launch, the first also draining the pipeline rows issued
+// ahead of the prologue.  The same terms in the same order: the same sums.
+__device__ __forceinline__ void cg_lane_partials(double (&S)[5], const double *__restrict__ part, int nb, int tid) {
+  constexpr int MT = PCG_MAX_BLOCKS / 256;
+  double t[MT][5];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int b = tid + m * 256, bc = b < nb ? b : 0;
+#pragma unroll
+    for (int v = 0; v < 5; ++v) t[m][v] = part[(size_t)v * PCG_MAX_BLOCKS + bc];
+  }
+#pragma unroll
+  for (int v = 0; v < 5; ++v) {
+    double s = 0.0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) s = tid + m * 256 < nb ? s + t[m][v] : s;
+    S[v] = s;
+  }
+}
+
 // Launch prologue of k_cg / k_cgs: fixed-order sum of the previous launch's
 // per-block partials (pq, qz, qMq, rz, rr) -> alpha_{k-1}, rho_k (CG
 // recurrence), beta_k, scipy's convergence test; the lead block records the
@@ -283,12 +307,9 @@ __device__ __forceinline__ bool cg_prologue(const PcgArgs &g, int k, double *lds
   // launch k-1's partials
   double S[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (!FIRST) {
+    cg_lane_partials(S, g.part_rd, g.nb, tid);
 #pragma unroll
-    for (int v = 0; v < 5; ++v) {
-      double s = 0.0;
-      for (int b = tid; b < g.nb; b += 256) s += g.part_rd[(size_t)v * PCG_MAX_BLOCKS + b];
-      S[v] = wave_sum(s);
-    }
+    for (int v = 0; v < 5; ++v) S[v] = wave_sum(S[v]);
     if ((tid & 63) == 0)
 #pragma unroll
       for (int v = 0; v < 5; ++v) lds[v * 8 + (tid >> 6)] = S[v];
@@ -2034,9 +2055,8 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   const int i0 = s * 64, i = i0 + lane;
   const bool rowok = i < H;
   const size_t ps = a.ps;
-  sorw_gf *gcf = (sorw_gf *)a.coef;
-  sorw_gf *gwxp = gcf + (PH ? 2 : 0) * ps, *gwyp = gcf + (PH ? 3 : 1) * ps;
-  sorw_gf *gdgp = gcf + (PH ? 6 : 4) * ps, *gccp = gcf + 5 * ps, *gbp = (sorw_gf *)a.b + PH;
+  const float *wxp = a.coef + (PH ? 2 : 0) * ps, *wyp = a.coef + (PH ? 3 : 1) * ps;
+  const float *dgp = a.coef + (PH ? 6 : 4) * ps, *ccp = a.coef + 5 * ps;
   const size_t row = (size_t)(rowok ? i : 0) * P;
   const bool has_up = s > 0, has_dn = i0 + 64 < H;
   const size_t row_up = (size_t)(has_up ? i0 - 1 : 0) * P, row_dn = (size_t)(has_dn ? i0 + 64 : 0) * P;
@@ -2056,77 +2076,60 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
   const float om = a.omega, om1 = 1.0f - a.omega;
   bool alive = true;
 
-  // Prefetch ring: raw values loaded unconditionally at clamped addresses,
-  // masked (+0 where the reference has no entry) at the step that uses them
-  // by an AND the compiler cannot see through (sorw_keep): a select it can
-  // see turns into a masked load whose value is waited for at once
-  // (s_waitcnt vmcnt(0): the whole prefetch drained every step).  The row
-  // above / below (lanes 0 / 63 only) is one address for the whole wave.
-  float X0[8], X1[8], XU[8], XD[8];
+  float2 X[8], XU[8], XD[8];
   float WX[8], WY[8], DG[8], CC[8], BB[8], WYU[8];
-  // The hand-off waits of a group of 8 steps' fetches (columns tp = t +
-  // SOR_D - lane for t in [t_lo, t_hi]) at once, before the group: a wait
-  // inside every step made each step ~650 instructions of control flow, and
-  // a poll (a global load) waits for every load issued before it.  Each wait
-  // is the per-column one of the largest column the group needs.
-  auto group_wait = [&](int t_lo, int t_hi) {
-    const int lo = t_lo + SOR_D, hi = t_hi + SOR_D;
-    const int a0 = max(lo, 0), bw = min(hi, W - 1), bn = min(hi, nsteps - 1);
-    if (has_up && a0 <= bw) alive = alive && sorp_wait(a, pup, base + bw + 64, known_up, k);
-    if (PH == 1 && a0 <= bn) alive = alive && sorp_wait(a, pu, base + bn + 1, known_u, k);
-    if (k > 0 && a0 <= bn) alive = alive && sorp_wait(a, pold, pbase + bn + 1, known_old, k);
-    const int d0 = max(lo - 63, 0), d1 = min(hi - 63, W - 1);
-    if (k > 0 && has_dn && d0 <= d1) alive = alive && sorp_wait(a, pdn, pbase + d1 + 1, known_dn, k);
-  };
-  auto fetch = [&](int t) {  // column t + SOR_D - lane (after group_wait)
+  auto fetch = [&](int t) {  // column t + SOR_D - lane
     const int tp = t + SOR_D, jp = tp - lane, q = tp & 7;
-    const size_t o = row + min(max(jp, 0), W - 1);
-    const float *xo = (const float *)(PH ? xc + o : xp + o);
-    X0[q] = sor_ld1(xo);
-    X1[q] = sor_ld1((const float *)(xp + o) + 1);
-    WX[q] = gwxp[o];
-    WY[q] = gwyp[o];
-    DG[q] = gdgp[o];
-    CC[q] = gccp[o];
-    BB[q] = gbp[2 * o];
-    const int ju = min(max(tp, 0), W - 1), jd = min(max(tp - 63, 0), W - 1);
-    XU[q] = sor_ld1((const float *)(xc + row_up + ju) + PH);
-    WYU[q] = gwyp[row_up + ju];
-    XD[q] = sor_ld1((const float *)(xp + row_dn + jd) + PH);
+    if (has_up && tp >= 0 && tp < W) alive = alive && sorp_wait(a, pup, base + tp + 64, known_up, k);
+    if (PH == 1 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pu, base + tp + 1, known_u, k);
+    if (k > 0 && tp >= 0 && tp < nsteps) alive = alive && sorp_wait(a, pold, pbase + tp + 1, known_old, k);
+    if (k > 0 && has_dn && tp - 63 >= 0 && tp - 63 < W)
+      alive = alive && sorp_wait(a, pdn, pbase + tp - 62, known_dn, k);
+    const bool ok = rowok && jp >= 0 && jp < W;
+    const size_t o = row + (ok ? jp : 0);
+    if (PH == 0) X[q] = ok ? sor_ld(xp + o) : make_float2(0.f, 0.f);
+    else X[q] = ok ? make_float2(sor_ld1((const float *)(xc + o)), sor_ld1((const float *)(xp + o) + 1))
+                   : make_float2(0.f, 0.f);
+    WX[q] = ok && jp + 1 < W ? wxp[o] : 0.f;
+    WY[q] = ok && i + 1 < H ? wyp[o] : 0.f;
+    DG[q] = ok ? sor_dg(dgp[o]) : 0.f;
+    CC[q] = ok ? ccp[o] : 0.f;
+    BB[q] = ok ? (PH ? a.b[o].y : a.b[o].x) : 0.f;
+    if (lane == 0) {
+      const bool u = has_up && jp >= 0 && jp < W;
+      XU[q] = u ? sor_ld(xc + row_up + jp) : make_float2(0.f, 0.f);
+      WYU[q] = u ? wyp[row_up + jp] : 0.f;
+    }
+    if (lane == 63) {
+      const bool d = has_dn && jp >= 0 && jp < W;
+      XD[q] = d ? sor_ld(xp + row_dn + jp) : make_float2(0.f, 0.f);
+    }
   };
-  group_wait(-SOR_D, -1);
-  if (!alive) return false;
 #pragma unroll
   for (int t = -SOR_D; t < 0; ++t) fetch(t);
+  if (!alive) return false;
 
   int stop_seen = 0x7fffffff;
   float res = 0.f, wx_prev = 0.f, wy_prev = 0.f;
-  // whole groups of 8 steps: the steps past nsteps relax nothing (every
-  // lane's column is past W) and store nothing
   for (int t0 = 0; t0 < nsteps; t0 += 8) {
-    group_wait(t0, t0 + 7);
-    if (!alive) return false;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = t0 + u;
+      if (t >= nsteps) break;
       fetch(t);
       const int j = t - lane, q = t & 7, q1 = (t + 1) & 7;
-      const bool act = rowok && j >= 0 && j < W, act1 = rowok && j + 1 >= 0 && j + 1 < W;
-      // X0 / X1: this half's component / the other one (PH 0: u, v; PH 1: v
-      // of the previous sweep in X1 and this sweep's u in X0)
-      const float old = sorw_keep(PH ? X1[q] : X0[q], act), other = sorw_keep(PH ? X0[q] : X1[q], act);
-      const float right = sorw_keep(PH ? X1[q1] : X0[q1], act1);
-      const float wxq = sorw_keep(WX[q], act && j + 1 < W), wyq = sorw_keep(WY[q], act && i + 1 < H);
-      const float dgq = sorw_keep(sor_dg(DG[q]), act), ccq = sorw_keep(CC[q], act), bbq = sorw_keep(BB[q], act);
+      const bool act = rowok && j >= 0 && j < W;
+      const float2 xo = X[q];
+      const float old = PH ? xo.y : xo.x, other = PH ? xo.x : xo.y;
+      const float right = PH ? X[q1].y : X[q1].x;
       float down = sor_from_down(right);
-      if (lane == 63) down = sorw_keep(XD[q], has_dn && j >= 0 && j < W);
+      if (lane == 63) down = PH ? XD[q].y : XD[q].x;
       float up = sor_from_up(res), wu = sor_from_up(wy_prev);
       if (lane == 0) {
-        const bool u = has_up && j >= 0 && j < W;
-        up = sorw_keep(XU[q], u);
-        wu = sorw_keep(WYU[q], u);
+        up = PH ? XU[q].y : XU[q].x;
+        wu = WYU[q];
       }
-      float nw = sor_relax(bbq, wx_prev, res, wxq, right, wyq, down, wu, up, ccq, other, dgq, old, om, om1);
+      float nw = sor_relax(BB[q], wx_prev, res, WX[q], right, WY[q], down, wu, up, CC[q], other, DG[q], old, om, om1);
       if (act) {
         const size_t o = row + j;
         sor_st(xc + o, PH ? make_float2(other, nw) : make_float2(nw, other));
@@ -2135,16 +2138,17 @@ __device__ __forceinline__ bool sorp_unit(const SorPipeArgs &a, int k, int s, do
         nw = 0.f;
       }
       res = nw;
-      wx_prev = wxq;
-      wy_prev = wyq;
+      wx_prev = act ? WX[q] : 0.f;
+      wy_prev = act ? WY[q] : 0.f;
+      if (((t + 1) & (SOR_G - 1)) == 0 || t + 1 == nsteps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(my, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // *stop as read at the previous publication (its load had a whole
+        // publication interval to return): abandon a sweep past the answer
+        if (stop_seen < k || !alive) return false;
+        stop_seen = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
+      }
     }
-    // publish the group (its sc1 stores drained first)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(my, base + min(t0 + 8, nsteps), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // *stop as read at the previous publication (its load had a whole
-    // publication interval to return): abandon a sweep past the answer
-    if (stop_seen < k) return false;
-    stop_seen = __builtin_amdgcn_readfirstlane(sor_poll(a.stop));
   }
   return alive;
 }
