@@ -179,6 +179,12 @@ struct HostStage {
 #define OF_SOR_PIPE_WAVES 512
 #endif
 // dynamic LDS of a k_sor_pipe wave (unused): bounds the waves per CU
+// k_sor_wg only where its ring holds >= OF_SORW_MIN_RING sweeps: at 60x80
+// (a ring of 3) it was slower than k_sor_pipe (37 vs 32 us per sweep), at
+// 30x40 (ring 8) faster (11 vs 26 us; profiles/r6e)
+#ifndef OF_SORW_MIN_RING
+#define OF_SORW_MIN_RING 8
+#endif
 // k_sor_wg's sweep ring in LDS (the rest of the 160 KB holds its stamps)
 #ifndef OF_SORW_RING_BYTES
 #define OF_SORW_RING_BYTES (144 * 1024)
@@ -1135,7 +1141,7 @@ SolveResult solve_impl(of_ctx *c, const of_params *P, const Img &coef, const F2 
   if (c->opt_sor_pipe == 2 && a.maxiter > 0 && H <= 64) {
     const size_t buf = sizeof(float2) * (size_t)H * W;
     const int S = (int)std::min<size_t>(SORW_MAXW, OF_SORW_RING_BYTES / buf);
-    if (S >= 2) {
+    if (S >= OF_SORW_MIN_RING) {
       SorWgArgs w;
       memset(&w, 0, sizeof(w));
       w.coef = coef.p;
