@@ -56,9 +56,22 @@ __host__ static inline PenF to_penf(const of_penalty &p) {
 // rho'(x)/x per kind (penalties.py d_type == 2); pen_k<K> picks one at
 // compile time (the assembly kernels specialised on the method's penalty
 // kinds), pen_w at run time -- the same arithmetic either way
+// OF_WARP_NOCONTRACT: no fma contraction in the warp / weight / assembly
+// arithmetic, so the fused warp + assembly and the two-kernel form round
+// every product and sum alike (A/B knob)
+#ifndef OF_WARP_NOCONTRACT
+#define OF_WARP_NOCONTRACT 0
+#endif
+#if OF_WARP_NOCONTRACT
+#define OF_NOCONTRACT _Pragma("clang fp contract(off)")
+#else
+#define OF_NOCONTRACT
+#endif
 __device__ __forceinline__ float pen_quad(const PenF &p, float) { return 2.0f / (p.p0 * p.p0); }
-__device__ __forceinline__ float pen_lorentz(const PenF &p, float x) { return 2.0f / (2.0f * p.p0 * p.p0 + x * x); }
+__device__ __forceinline__ float pen_lorentz(const PenF &p, float x) {
+  OF_NOCONTRACT return 2.0f / (2.0f * p.p0 * p.p0 + x * x); }
 __device__ __forceinline__ float pen_charb(const PenF &p, float x) {
+  OF_NOCONTRACT
   float s2 = p.p0 * p.p0, t = x / s2;
   return 1.0f / (s2 * sqrtf(1.0f + t * t));
 }
@@ -66,9 +79,11 @@ __device__ __forceinline__ float pen_charb(const PenF &p, float x) {
 // positive float (sigma^2 + x^2 >= sigma^2), so the hardware v_log_f32 /
 // v_exp_f32 pair (~1 ulp each) replaces the ~30-instruction general powf
 __device__ __forceinline__ float pen_gcharb(const PenF &p, float x) {
+  OF_NOCONTRACT
   return 2.0f * p.p1 * __builtin_amdgcn_exp2f((p.p1 - 1.0f) * __builtin_amdgcn_logf(p.p0 * p.p0 + x * x));
 }
 __device__ __forceinline__ float pen_w(const PenF &p, float x) {
+  OF_NOCONTRACT
   switch (p.kind) {
     case OF_PEN_QUADRATIC: return pen_quad(p, x);
     case OF_PEN_LORENTZIAN: return pen_lorentz(p, x);
@@ -94,6 +109,7 @@ __device__ __forceinline__ float pen_w(const PenF &p, float x) {
 }
 template <int K>
 __device__ __forceinline__ float pen_k(const PenF &p, float x) {
+  OF_NOCONTRACT
   if constexpr (K == OF_PEN_QUADRATIC) return pen_quad(p, x);
   else if constexpr (K == OF_PEN_LORENTZIAN) return pen_lorentz(p, x);
   else if constexpr (K == OF_PEN_CHARBONNIER) return pen_charb(p, x);

@@ -8,6 +8,7 @@
 // cubic Hermite basis (tensor-product form of derivatives.py:7-24's
 // 16x16 bicubic coefficient matrix)
 __device__ __forceinline__ void hermite(float t, float h[4], float dh[4]) {
+  OF_NOCONTRACT
   float t2 = t * t, t3 = t2 * t;
   h[0] = 2.0f * t3 - 3.0f * t2 + 1.0f;
   h[1] = -2.0f * t3 + 3.0f * t2;
@@ -20,6 +21,7 @@ __device__ __forceinline__ void hermite(float t, float h[4], float dh[4]) {
 }
 
 __device__ __forceinline__ float bspline3(float t) {
+  OF_NOCONTRACT
   t = fabsf(t);
   if (t < 1.0f) return 2.0f / 3.0f - t * t + 0.5f * t * t * t;
   if (t < 2.0f) {
@@ -56,6 +58,7 @@ struct RegOut {
 template <int INTERP, int NC, typename Out>
 __device__ __forceinline__ void warp_pixel(const DerivArgs &d, int H, int W, int P, size_t ps, int i, int j, float x2,
                                            float y2, Out &out) {
+  OF_NOCONTRACT
   const size_t k = (size_t)i * P + j;
   const int nc = NC > 0 ? NC : d.nc;
   if (INTERP == OF_INTERP_BICUBIC) {
@@ -185,6 +188,7 @@ struct PenMode {
 
 template <int M = OF_PM_ANY>
 __device__ __forceinline__ float2 edge_w(const OpArgs &o, int axis, float du, float dv) {
+  OF_NOCONTRACT
   using PM = PenMode<M>;
   float wu = 0.0f, wv = 0.0f;
   if (PM::q(o)) { wu += o.aq_s * PM::pen(o.qsu[axis], du); wv += o.aq_s * PM::pen(o.qsv[axis], dv); }
@@ -206,6 +210,7 @@ __device__ __forceinline__ void assemble_px(const OpArgs &o, const float2 *__res
                                             const float2 *__restrict__ duv, int nc_rt, const float2 *__restrict__ uvhat,
                                             int i, int j, int H, int W, int P, size_t ps, float *__restrict__ coef,
                                             float2 *__restrict__ rhs, const Deriv &deriv) {
+  OF_NOCONTRACT
   using PM = PenMode<M>;
   const int nc = NC > 0 ? NC : nc_rt;
   const size_t k = (size_t)i * P + j;
@@ -574,6 +579,11 @@ extern __device__ unsigned long long g_wmf_t[];
 // chunks per list of the large regions (>= 512 keys, area_hsz >= 7): 16
 // halves the crossing-chunk walk (32 samples per list instead of 64) for
 // twice the chunk-sum LDS (16 KB per wave: 5 instead of 8 waves per CU)
+// WMF_ROWACC: per row, the weights of the middle sample's chunk summed in a
+// register and added to LDS once (A/B knob; off: every weight is one LDS add)
+#ifndef WMF_ROWACC
+#define WMF_ROWACC 0
+#endif
 #ifndef WMF_NC_BIG
 #define WMF_NC_BIG 8
 #endif
@@ -969,6 +979,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
           cv[dx] = cid[RW * RP + q0 + dx];
         }
       }
+#if WMF_ROWACC
+    // one register accumulator per list and row for the chunk of the row's
+    // middle sample (a smooth flow keeps most of a row's samples in one
+    // chunk): those weights are summed in registers and added to LDS once
+    // at the row's end; the others are added to LDS as they come
+    if (HS > 0) {
+      constexpr int MID = MX / 2;
+      const unsigned ku = cu[MID], kv = cv[MID];
+      wmf_sum_t au = 0.0, av = 0.0;
+#pragma unroll
+      for (int dx = 0; dx < MX; ++dx) {
+        const wmf_sum_t w = (wmf_sum_t)wmf_w(rec[dx], c01, cg[2], nk);
+        const bool mu = cu[dx] == ku, mv = cv[dx] == kv;
+        au += mu ? w : (wmf_sum_t)0.0;
+        av += mv ? w : (wmf_sum_t)0.0;
+        if (!mu) atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cu[dx] << WMF_SUM_SHIFT)), w);
+        if (!mv) atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + NC * 64, w);
+      }
+      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (ku << WMF_SUM_SHIFT)), au);
+      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (kv << WMF_SUM_SHIFT)) + NC * 64, av);
+      return;
+    }
+#endif
 #pragma unroll
     for (int dx = 0; dx < MX; ++dx)
       if (dx < n) {
