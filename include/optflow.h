@@ -167,10 +167,11 @@ int of_synchronize(of_ctx *ctx);
  * axis across the batch lanes (of_kernel_timeline); see of_kernel_times */
 int of_set_profiling(of_ctx *ctx, int enable);
 /* solver options of a context (inherited by its batch lanes):
- *   OF_OPT_SOR_PIPELINE  1 (default): 'sor' runs its sweeps pipelined in one
- *                        persistent launch (k_sor_pipe); 2: as 1, and levels
- *                        of <= 64 rows whose sweep ring fits in LDS run in
- *                        one workgroup (k_sor_wg); 0: one launch per sweep
+ *   OF_OPT_SOR_PIPELINE  2 (default): 'sor' runs its sweeps pipelined in one
+ *                        persistent launch (k_sor_pipe), and a level of <= 64
+ *                        rows whose LDS ring holds >= 8 sweeps in one
+ *                        workgroup (k_sor_wg); 1: k_sor_pipe only; 0: one
+ *                        launch per sweep
  *                        (k_sor_lex).  All give the same iterate and sweep
  *                        count bitwise. */
 #define OF_OPT_SOR_PIPELINE 1

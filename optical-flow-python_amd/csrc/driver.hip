@@ -255,7 +255,9 @@ struct of_ctx {
   int prog_stage = 0, prog_level = -1;
   std::chrono::steady_clock::time_point prog_t0;
   std::vector<float> prog_uv;  // host copy of a stage's flow (OF_PROGRESS_FLOW)
-  int opt_sor_pipe = 1;    // of_set_option(OF_OPT_SOR_PIPELINE)
+  // of_set_option(OF_OPT_SOR_PIPELINE): 2 (default) = k_sor_pipe, and
+  // k_sor_wg where its LDS ring holds >= OF_SORW_MIN_RING sweeps
+  int opt_sor_pipe = 2;
   int opt_fused_warp = OF_FUSED_WARP_DEFAULT;  // of_set_option(OF_OPT_FUSED_WARP)
   // solve log (of_set_solve_log): fp64 true residual of every solve
   int slog = 0;

@@ -198,7 +198,7 @@ def _sor_both(fn):
         ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
         return fn(), ref
     finally:
-        ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 2)  # the default
 
 
 @pytest.mark.parametrize("H,W,maxit", [(40, 56, 10000), (64, 64, 10000), (150, 200, 10000), (300, 90, 10000),
@@ -253,7 +253,7 @@ def _sor_modes(fn, modes=(0, 2)):
             ran.append({names[i].decode() for i in range(min(n.value, 256))})
             ctx.check(ctx.lib.of_set_profiling(ctx.handle, 0))
     finally:
-        ctx.set_option(OF_OPT_SOR_PIPELINE, 1)
+        ctx.set_option(OF_OPT_SOR_PIPELINE, 2)  # the default
     return out, ran
 
 
