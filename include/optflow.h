@@ -178,11 +178,9 @@ int of_set_profiling(of_ctx *ctx, int enable);
 /*   OF_OPT_FUSED_WARP    1 (default): each warping iteration's partial_deriv
  *                        and flow_operator run as one kernel (no It / Ix /
  *                        Iy planes; 1 or 3 channels, one linearisation per
- *                        warp); 0: two kernels.  The same system up to fp32
- *                        rounding: the compiler contracts different products
- *                        into fma in the two forms, so the planes agree to
- *                        the family tolerance, not bitwise
- *                        (tests/test_gpu_stages.py). */
+ *                        warp); 0: two kernels.  The same system bitwise
+ *                        (no fma contraction in either form's warp, weight
+ *                        and assembly arithmetic; tests/test_gpu_stages.py). */
 #define OF_OPT_FUSED_WARP 3
 int of_set_option(of_ctx *ctx, int option, int value);
 /* read an option, or a read-only counter of the context and its batch lanes:

@@ -56,11 +56,14 @@ __host__ static inline PenF to_penf(const of_penalty &p) {
 // rho'(x)/x per kind (penalties.py d_type == 2); pen_k<K> picks one at
 // compile time (the assembly kernels specialised on the method's penalty
 // kinds), pen_w at run time -- the same arithmetic either way
-// OF_WARP_NOCONTRACT: no fma contraction in the warp / weight / assembly
-// arithmetic, so the fused warp + assembly and the two-kernel form round
-// every product and sum alike (A/B knob)
+// OF_WARP_NOCONTRACT (default 1): no fma contraction in the warp / weight /
+// assembly arithmetic, so the fused warp + assembly and the two-kernel form
+// round every product and sum alike and assemble the same system bitwise
+// (left to the compiler the two forms contracted different products; round
+// 6, profiles/r6k: the smoke pair's mean |uv - oracle| 3.69e-3 -> 6.7e-4,
+// every parity test green, -0.7 % pairs/s)
 #ifndef OF_WARP_NOCONTRACT
-#define OF_WARP_NOCONTRACT 0
+#define OF_WARP_NOCONTRACT 1
 #endif
 #if OF_WARP_NOCONTRACT
 #define OF_NOCONTRACT _Pragma("clang fp contract(off)")

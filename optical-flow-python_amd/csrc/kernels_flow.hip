@@ -202,24 +202,48 @@ __device__ __forceinline__ float2 ld_uvd(const float2 *uv, const float2 *duv, si
   return a;
 }
 
+// The flow at a pixel and its four neighbours, loaded together at clamped
+// indices (a neighbour outside the image reads the pixel itself; its value
+// is never used) and pinned in registers right away: loaded under the
+// boundary branches, each load was a masked load waited for on its own --
+// four more memory round trips per pixel row of the fused warp + assembly,
+// after the gather's.
+struct UvNbr {
+  float2 c, r, d, l, u;
+};
+__device__ __forceinline__ UvNbr ld_nbr(const float2 *__restrict__ uv, int i, int j, int H, int W, int P) {
+  const size_t k = (size_t)i * P + j;
+  UvNbr n;
+  n.c = uv[k];
+  n.r = uv[j < W - 1 ? k + 1 : k];
+  n.d = uv[i < H - 1 ? k + P : k];
+  n.l = uv[j > 0 ? k - 1 : k];
+  n.u = uv[i > 0 ? k - P : k];
+  asm volatile("" : "+v"(n.c.x), "+v"(n.c.y), "+v"(n.r.x), "+v"(n.r.y), "+v"(n.d.x), "+v"(n.d.y), "+v"(n.l.x),
+               "+v"(n.l.y), "+v"(n.u.x), "+v"(n.u.y));
+  return n;
+}
+
 // coef planes: 0 wx_u, 1 wy_u, 2 wx_v, 3 wy_v, 4 a_uu, 5 a_uv, 6 a_vv; rhs float2.
 // One pixel's row of the system; deriv(ch, It, Ix, Iy) fetches channel ch's
-// derivatives (planes, or the fused kernel's registers).
+// derivatives (planes, or the fused kernel's registers).  nb: the flow of
+// the pixel and its neighbours already in registers (ld_nbr; only without
+// duv), else loaded here.
 template <int NC, int M, typename Deriv>
 __device__ __forceinline__ void assemble_px(const OpArgs &o, const float2 *__restrict__ uv,
                                             const float2 *__restrict__ duv, int nc_rt, const float2 *__restrict__ uvhat,
                                             int i, int j, int H, int W, int P, size_t ps, float *__restrict__ coef,
-                                            float2 *__restrict__ rhs, const Deriv &deriv) {
+                                            float2 *__restrict__ rhs, const Deriv &deriv, const UvNbr *nb = nullptr) {
   OF_NOCONTRACT
   using PM = PenMode<M>;
   const int nc = NC > 0 ? NC : nc_rt;
   const size_t k = (size_t)i * P + j;
-  const float2 c = ld_uvd(uv, duv, k);
+  const float2 c = nb ? nb->c : ld_uvd(uv, duv, k);
   float2 eR = make_float2(0.f, 0.f), eD = eR, eL = eR, eU = eR;
-  if (j < W - 1) { float2 n = ld_uvd(uv, duv, k + 1); eR = edge_w<M>(o, 0, n.x - c.x, n.y - c.y); }
-  if (i < H - 1) { float2 n = ld_uvd(uv, duv, k + P); eD = edge_w<M>(o, 1, n.x - c.x, n.y - c.y); }
-  if (j > 0) { float2 n = ld_uvd(uv, duv, k - 1); eL = edge_w<M>(o, 0, c.x - n.x, c.y - n.y); }
-  if (i > 0) { float2 n = ld_uvd(uv, duv, k - P); eU = edge_w<M>(o, 1, c.x - n.x, c.y - n.y); }
+  if (j < W - 1) { float2 n = nb ? nb->r : ld_uvd(uv, duv, k + 1); eR = edge_w<M>(o, 0, n.x - c.x, n.y - c.y); }
+  if (i < H - 1) { float2 n = nb ? nb->d : ld_uvd(uv, duv, k + P); eD = edge_w<M>(o, 1, n.x - c.x, n.y - c.y); }
+  if (j > 0) { float2 n = nb ? nb->l : ld_uvd(uv, duv, k - 1); eL = edge_w<M>(o, 0, c.x - n.x, c.y - n.y); }
+  if (i > 0) { float2 n = nb ? nb->u : ld_uvd(uv, duv, k - P); eU = edge_w<M>(o, 1, c.x - n.x, c.y - n.y); }
   // data term, channel-averaged (classic_nl.py:330-343)
   float du = 0.f, dv = 0.f;
   if (duv) { du = duv[k].x; dv = duv[k].y; }
@@ -238,12 +262,12 @@ __device__ __forceinline__ void assemble_px(const OpArgs &o, const float2 *__res
   const float psi = ((PM::q(o) ? o.aq_d * psq : 0.f) + (PM::r(o) ? o.ar_d * psr : 0.f)) * inv;
   ix2 *= inv; iy2 *= inv; ixy *= inv; itx *= inv; ity *= inv;
   // b uses uv (not uv + duv): classic_nl.py:362-367
-  const float2 u0 = uv[k];
+  const float2 u0 = nb ? nb->c : uv[k];
   float lu = 0.f, lv = 0.f;
-  if (j < W - 1) { float2 n = uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
-  if (i < H - 1) { float2 n = uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
-  if (j > 0) { float2 n = uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
-  if (i > 0) { float2 n = uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
+  if (j < W - 1) { float2 n = nb ? nb->r : uv[k + 1]; lu += eR.x * (u0.x - n.x); lv += eR.y * (u0.y - n.y); }
+  if (i < H - 1) { float2 n = nb ? nb->d : uv[k + P]; lu += eD.x * (u0.x - n.x); lv += eD.y * (u0.y - n.y); }
+  if (j > 0) { float2 n = nb ? nb->l : uv[k - 1]; lu += eL.x * (u0.x - n.x); lv += eL.y * (u0.y - n.y); }
+  if (i > 0) { float2 n = nb ? nb->u : uv[k - P]; lu += eU.x * (u0.x - n.x); lv += eU.y * (u0.y - n.y); }
   float auu = psi * ix2 + (eL.x + eR.x + eU.x + eD.x);
   float avv = psi * iy2 + (eL.y + eR.y + eU.y + eD.y);
   float bu = -lu - psi * itx, bv = -lv - psi * ity;
@@ -285,17 +309,19 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_flow_operator(OpArgs o, const 
 // Warp + derivatives + assembly in one pass: the
 // per-channel It / Ix / Iy of a pixel stay in registers, so the 24 B/px
 // round trip of the three planes (nc = 1) and one launch per warping
-// iteration go away.  The same formulas as k_partial_deriv + k_flow_operator;
-// the compiler contracts different products into fma in the two forms, so
-// the planes agree to fp32 rounding (tests/test_gpu_stages.py), not bitwise.
+// iteration go away.  The same arithmetic as k_partial_deriv +
+// k_flow_operator, bitwise: no fma contraction in either (OF_WARP_NOCONTRACT;
+// tests/test_gpu_stages.py).
 template <int INTERP, int NC, int M>
 __global__ __launch_bounds__(OF_BX *OF_BY) void k_warp_operator(DerivArgs d, OpArgs o, const float2 *__restrict__ uv,
                                                                 int H, int W, int P, size_t ps,
                                                                 float *__restrict__ coef, float2 *__restrict__ rhs) {
   OF_FOR_PIXELS_XCD(H, W) {
     if (j >= W) continue;
-    const size_t k = (size_t)i * P + j;
-    const float2 f = uv[k];
+    // the pixel's and its neighbours' flow in one round trip, before the
+    // gather that needs the pixel's
+    const UvNbr nb = ld_nbr(uv, i, j, H, W, P);
+    const float2 f = nb.c;
     RegOut<NC> r;
     warp_pixel<INTERP, NC>(d, H, W, P, ps, i, j, (float)(j + 1) + f.x, (float)(i + 1) + f.y, r);
     assemble_px<NC, M>(o, uv, (const float2 *)nullptr, NC, (const float2 *)nullptr, i, j, H, W, P, ps, coef, rhs,
@@ -303,7 +329,7 @@ __global__ __launch_bounds__(OF_BX *OF_BY) void k_warp_operator(DerivArgs d, OpA
                       it = r.it[ch];
                       gx = r.ix[ch];
                       gy = r.iy[ch];
-                    });
+                    }, &nb);
   }
 }
 #define OF_WOP(I, N, M) template __global__ void k_warp_operator<I, N, M>(DerivArgs, OpArgs, const float2 *, int, int, \

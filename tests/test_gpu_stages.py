@@ -458,12 +458,11 @@ def test_solve_rtol0_stops_at_noise_floor(H, W):
 def test_fused_warp_operator_matches_two_kernels(golden, method):
     """The fused warp + assembly (k_warp_operator, OF_OPT_FUSED_WARP = 1, the
     default) and partial_deriv + flow_operator as two kernels compute the
-    same system; the compiler contracts a few products into fma differently
-    in the two kernels, so the flows agree to rounding, amplified by the
-    IRLS / median steps as any last-bit change is (measured max |diff|: HS
-    1.1e-4, BA 5.8e-5, Classic+NL-fast 1.4e-4 px; the chaotic family more).
-    Both meet the e2e parity gates against the reference (test_gpu_e2e's TOL),
-    and their mutual mean difference is within the family's tolerance."""
+    same system bitwise: neither form contracts products into fma
+    (OF_WARP_NOCONTRACT, round 6; before, the two forms contracted
+    different products and the flows differed by up to 1.4e-4 px), so the
+    flows are bitwise equal; both meet the e2e parity gates against the
+    reference (test_gpu_e2e's TOL)."""
     import optical_flow
     from optical_flow import _abi, _native
     from test_gpu_e2e import FAMILY, TOL
@@ -480,7 +479,7 @@ def test_fused_warp_operator_matches_two_kernels(golden, method):
     mean_tol, med_tol = TOL[FAMILY[method]]
     s = epe_stats(fused, two)
     print(method, "fused vs two kernels", s, "bitwise", bool(np.array_equal(fused, two)))
-    assert s["mean"] < mean_tol and s["median"] < med_tol
+    np.testing.assert_array_equal(fused, two)
     for uv in (fused, two):
         r = epe_stats(uv, d[method])
         assert r["mean"] < mean_tol and r["median"] < med_tol, r
