@@ -602,18 +602,11 @@ extern __device__ unsigned long long g_wmf_t[];
 #define WMF_STAMP(i)
 #endif
 #define WMF_NC 8
-// chunks per list of the large regions (>= 512 keys, area_hsz >= 7): 16
-// halves the crossing-chunk walk (32 samples per list instead of 64) for
-// twice the chunk-sum LDS (16 KB per wave: 5 instead of 8 waves per CU)
-// WMF_ROWACC: per row, the weights of the middle sample's chunk summed in a
-// register and added to LDS once (A/B knob; off: every weight is one LDS add)
-#ifndef WMF_ROWACC
-#define WMF_ROWACC 0
-#endif
-#ifndef WMF_NC_BIG
-#define WMF_NC_BIG 8
-#endif
-__host__ __device__ constexpr int wmf_nc(int nkeys) { return nkeys >= 512 ? WMF_NC_BIG : WMF_NC; }
+// (measured round 6 and removed: 16 chunks for the large regions, 0.888 vs
+// 0.691 ms per 1080p launch at 5 instead of 8 waves per CU; a register
+// accumulator per row for the middle sample's chunk, 0.828 vs 0.692 ms --
+// DESIGN.md "Round 6 in brief" item 4)
+__host__ __device__ constexpr int wmf_nc(int) { return WMF_NC; }
 // WMF_CID_PAIR: the u- and v-list chunk ids of a region sample side by side
 // ([RW][RP][2] u8, one u16 read per window sample) instead of two planes
 // ([2][RW][RP] u8, two u8 reads)
@@ -1005,29 +998,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
           cv[dx] = cid[RW * RP + q0 + dx];
         }
       }
-#if WMF_ROWACC
-    // one register accumulator per list and row for the chunk of the row's
-    // middle sample (a smooth flow keeps most of a row's samples in one
-    // chunk): those weights are summed in registers and added to LDS once
-    // at the row's end; the others are added to LDS as they come
-    if (HS > 0) {
-      constexpr int MID = MX / 2;
-      const unsigned ku = cu[MID], kv = cv[MID];
-      wmf_sum_t au = 0.0, av = 0.0;
-#pragma unroll
-      for (int dx = 0; dx < MX; ++dx) {
-        const wmf_sum_t w = (wmf_sum_t)wmf_w(rec[dx], c01, cg[2], nk);
-        const bool mu = cu[dx] == ku, mv = cv[dx] == kv;
-        au += mu ? w : (wmf_sum_t)0.0;
-        av += mv ? w : (wmf_sum_t)0.0;
-        if (!mu) atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cu[dx] << WMF_SUM_SHIFT)), w);
-        if (!mv) atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (cv[dx] << WMF_SUM_SHIFT)) + NC * 64, w);
-      }
-      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (ku << WMF_SUM_SHIFT)), au);
-      atomicAdd(reinterpret_cast<wmf_sum_t *>(csb + (kv << WMF_SUM_SHIFT)) + NC * 64, av);
-      return;
-    }
-#endif
 #pragma unroll
     for (int dx = 0; dx < MX; ++dx)
       if (dx < n) {
