@@ -13,10 +13,21 @@ sys.path.insert(0, __import__("os").path.dirname(__file__))
 from isa_census import disassemble  # noqa: E402
 
 
+def _canon(lines):
+    # --symbolize-operands numbers branch labels across the whole object:
+    # renumber them per kernel in order of first use
+    ids = {}
+    sub = lambda m: "L%d" % ids.setdefault(m.group(0), len(ids))
+    return [re.sub(r"\bL\d+\b", sub, ln) for ln in lines]
+
+
 def kernels(lib):
     out, name = {}, None
     for ln in disassemble(lib).splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", ln)
+        if m and re.fullmatch(r"L\d+", m.group(1)) and name:
+            out[name].append(m.group(1) + ":")  # a branch label inside the kernel
+            continue
         if m:
             name = m.group(1)
             out[name] = []
@@ -24,7 +35,7 @@ def kernels(lib):
         if name and ln.startswith("\t"):
             # drop the address / encoding comment, keep the instruction text
             out[name].append(ln.split("//")[0].strip())
-    return out
+    return {k: _canon(v) for k, v in out.items()}
 
 
 def main(a, b):
