@@ -607,6 +607,12 @@ extern __device__ unsigned long long g_wmf_t[];
 // accumulator per row for the middle sample's chunk, 0.828 vs 0.692 ms --
 // DESIGN.md "Round 6 in brief" item 4)
 __host__ __device__ constexpr int wmf_nc(int) { return WMF_NC; }
+// WMF_WALK_LAST: the crossing sample found as the last one whose preceding
+// sum is below half (1) or the first whose sum reaches half (0); the same
+// sample either way (see the walk)
+#ifndef WMF_WALK_LAST
+#define WMF_WALK_LAST 1
+#endif
 // WMF_CID_PAIR: the u- and v-list chunk ids of a region sample side by side
 // ([RW][RP][2] u8, one u16 read per window sample) instead of two planes
 // ([2][RW][RP] u8, two u8 reads)
@@ -1042,8 +1048,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   WMF_STAMP(4);
   const unsigned span = 2u * hsz;
   // walk results as record indices relative to the lane's window origin qb
-  // (0xffff: none yet)
-  unsigned resu = 0xffffu, resv = 0xffffu, lstu = 0, lstv = 0;
+#if WMF_WALK_LAST
+  // The median is the first in-window sample whose cumulative sum reaches
+  // half; every in-window weight is >= 1e-10 (far above an ulp of a sum
+  // <= 225), so the sums strictly increase and that sample is also the LAST
+  // in-window sample whose sum BEFORE it is still below half (the walk starts
+  // below half: the crossing chunk's prefix, or the fallback's).  With no
+  // crossing in the chunk that is its last in-window sample -- the fallback
+  // below -- so one compare and one select per sample and list, no "found"
+  // state (the same sample bitwise; the first-reach form: WMF_WALK_LAST 0)
+  unsigned resu = 0, resv = 0;
+#else
+  unsigned resu = 0xffffu, resv = 0xffffu, lstu = 0, lstv = 0;  // 0xffff: none yet
+#endif
   // the crossing chunks' sorted positions (ry << 8 | rx), 8 per 16-B read;
   // window offsets straight from the position bytes (dy = ry - py and
   // dx = rx - px as unsigned: out of the window unless both <= span; padding
@@ -1073,20 +1090,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float xa = wmf_w(ra[i], c01, cg[2], nk), xb = wmf_w(rb[i], c01, cg[2], nk);
+#if WMF_WALK_LAST
+      resu = (ina[i] && bu < half) ? qa[i] : resu;
+      resv = (inb[i] && bv < half) ? qv[i] : resv;
+#endif
       bu += (double)(ina[i] ? xa : 0.f);  // select before the widening: one v_cndmask
       bv += (double)(inb[i] ? xb : 0.f);
+#if !WMF_WALK_LAST
       resu = (resu == 0xffffu && ina[i] && bu >= half) ? qa[i] : resu;
       resv = (resv == 0xffffu && inb[i] && bv >= half) ? qv[i] : resv;
       lstu = ina[i] ? qa[i] : lstu;
       lstv = inb[i] ? qv[i] : lstv;
+#endif
     }
     // (measured r5v: a wave-level exit once every lane has both medians,
     // `if (!__any(resu == 0xffff || resv == 0xffff)) break;`, is 1.5 % slower
     // per launch, 0.812 vs 0.801 ms, same flow: the walk is short and the
     // vote costs more than the samples it saves)
   }
+#if !WMF_WALK_LAST
   if (resu == 0xffffu) resu = lstu;
   if (resv == 0xffffu) resv = lstv;
+#endif
   WMF_STAMP(5);
   if (gi < H && gj < W) {
     // the selected samples' values, re-read at their (mirrored) positions
