@@ -714,6 +714,29 @@ __device__ __forceinline__ void swap_lane64(uint64_t v, int lj, uint64_t &a, uin
   b = ((uint64_t)bhi << 32) | blo;
 }
 
+// v_permlane16_swap / v_permlane32_swap of two 64-bit registers: the upper
+// row of each 32-lane row pair (lj = 16) / the upper 32 lanes (lj = 32) of x
+// trade places with the lower row / half of y, i.e. afterwards lower lanes
+// hold (x own, x of lane + lj) and upper lanes (y of lane - lj, y own)
+__device__ __forceinline__ void swap_rows64(uint64_t &x, uint64_t &y, int lj) {
+  const unsigned xl = (unsigned)x, xh = (unsigned)(x >> 32), yl = (unsigned)y, yh = (unsigned)(y >> 32);
+  unsigned a0, a1, b0, b1;
+  if (lj == 16) {
+    const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+    a0 = l[0]; b0 = l[1]; a1 = h[0]; b1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    a0 = l[0]; b0 = l[1]; a1 = h[0]; b1 = h[1];
+  }
+  x = ((uint64_t)a1 << 32) | a0;
+  y = ((uint64_t)b1 << 32) | b0;
+}
+#ifndef WMF_SWAP_PAIR
+#define WMF_SWAP_PAIR 1
+#endif
+
 // Sort keys: the flow value widened to fp64 (exact), the region position
 // (ry << 8 | rx) in the 29 mantissa bits the widening leaves zero.  As
 // doubles they order by value, ties by position (reversed for negative
@@ -791,6 +814,23 @@ struct Bitonic {
     if constexpr (JJ >= NPER) {
       constexpr int lj = JJ / NPER;
       if constexpr (lj == 16 || lj == 32) {
+#if WMF_SWAP_PAIR
+        // the two lists' key r in one exchange: swap_rows64(a, b) leaves the
+        // lower rows / half holding list a's pair (own, partner) and the upper
+        // ones list b's pair; each lane forms (min, max) of its pair, and the
+        // same exchange of (min, max) hands every lane its own result -- list
+        // a: lower min, upper max; list b likewise -- in 3 instructions per
+        // key instead of 2 copies + 2 swaps + min + max + 2 selects
+#pragma unroll
+        for (int r = 0; r < NPER; ++r) {
+          uint64_t x = ka[r], y = kb[r], mn, mx;
+          swap_rows64(x, y, lj);
+          wmf_minmax(x, y, mn, mx);
+          swap_rows64(mn, mx, lj);
+          ka[r] = mn;
+          kb[r] = mx;
+        }
+#else
         const bool take_min = (lane & lj) == 0;
 #pragma unroll
         for (int r = 0; r < NPER; ++r) {
@@ -802,6 +842,7 @@ struct Bitonic {
           ka[r] = take_min ? an : ax;
           kb[r] = take_min ? bn : bx;
         }
+#endif
       } else {
         // every partner first, then the minima: the DPP moves of a key are
         // not right behind the v_xor that wrote it (VALU -> DPP hazard nops)
@@ -1094,8 +1135,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       resu = (ina[i] && bu < half) ? qa[i] : resu;
       resv = (inb[i] && bv < half) ? qv[i] : resv;
 #endif
-      bu += (double)(ina[i] ? xa : 0.f);  // select before the widening: one v_cndmask
-      bv += (double)(inb[i] ? xb : 0.f);
+      // select before the widening: one v_cndmask instead of two (the empty
+      // asm keeps the compiler from hoisting the conversion above the select)
+      float sa = ina[i] ? xa : 0.f, sb = inb[i] ? xb : 0.f;
+      asm("" : "+v"(sa), "+v"(sb));
+      bu += (double)sa;
+      bv += (double)sb;
 #if !WMF_WALK_LAST
       resu = (resu == 0xffffu && ina[i] && bu >= half) ? qa[i] : resu;
       resv = (resv == 0xffffu && inb[i] && bv >= half) ? qv[i] : resv;
