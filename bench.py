@@ -94,14 +94,14 @@ KERNEL_BYTES_PER_PX = {
 CLOCK_HZ = 2.4e9
 VALU_ISSUE_PEAK = 256 * 4 * 0.5 * CLOCK_HZ
 # the weighted median's per-phase ISA census priced by measured issue costs
-WMF_CENSUS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5_wmf_census.json")
+WMF_CENSUS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r6_wmf_census.json")
 
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=8, help="pairs per GPU per step (config 5: 64 pairs / 8 GPUs)")
     ap.add_argument("--lanes", type=int, default=4, help="concurrent pair pipelines per GPU (of_pairs_run_host)")
     ap.add_argument("--height", type=int, default=1080)
@@ -318,7 +318,7 @@ def wmf_compute_roofline(per_level):
     """The weighted median is not HBM bound: `frac` = the
     VALU SIMD-cycles its instructions occupy (tools/isa_census.py: the
     shipped ISA per phase, each opcode at its measured issue cost,
-    profiles/r5_wmf_census.json) over the finest-level launch's mean duration
+    profiles/r6_wmf_census.json) over the finest-level launch's mean duration
     in the isolated replay x 1024 SIMDs x clock.  Beside it the PMC
     instruction rate against a 2-cycle issue (`insts_frac_2cyc`, which
     understates fp64 / transcendental / DPP instructions) and `hbm_frac`."""
