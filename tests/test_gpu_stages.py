@@ -336,7 +336,10 @@ def test_weighted_median(golden, guide, hsz, sig, key):
     assert same.mean() >= 0.999, same.mean()
 
 
-@pytest.mark.parametrize("gc,hsz,sig", [(3, 7, 7.0), (1, 7, 7.0), (3, 3, 4.0), (3, 12, 7.0)])
+# sort keys per lane (NPER) by window: hsz 0 -> 1, 1 -> 2, 3 -> 4, 5 / 7 -> 8
+# (7: the compile-time instance), 12 -> 16 -- every k_wmf instance's sort
+@pytest.mark.parametrize("gc,hsz,sig", [(3, 7, 7.0), (1, 7, 7.0), (3, 3, 4.0), (3, 12, 7.0), (3, 0, 7.0),
+                                        (3, 1, 7.0), (1, 1, 7.0), (3, 5, 7.0)])
 def test_weighted_median_synthetic_vs_oracle(gc, hsz, sig):
     """Weighted median of a 96x136 synthetic flow (smooth field + noise +
     a motion edge, so sorted chunks and window crossings vary) against the
